@@ -1,0 +1,504 @@
+// MI355X (gfx950) GAT attention layer: HIP kernels + C-ABI.
+//
+// Replaces the hot path of danieldritter/ATMLGraphAttentionNetworks
+// GraphAttentionLayer.forward (GAT.py:37-67) and the PyG pieces it calls:
+//   gat_csr_build       <- utils.add_self_loops (GAT.py:38) + propagate's
+//                          grouping of edges by edge_index[1] (GAT.py:53)
+//   gat_project         <- the per-head Linear loop + attention Linears
+//                          (GAT.py:42-52), one fp32 MFMA GEMM with a fused
+//                          score epilogue
+//   gat_edge_aggregate  <- propagate/message/softmax/aggregate + bias
+//                          (GAT.py:53-67, PyG utils.softmax, aggr='add')
+//
+// Data layout in HBM (see DESIGN.md "Data layout"):
+//   node table T[n_nodes][ld] fp32, one row per SOURCE node:
+//       [0, HF)        Wh = x W^T + b   (head-major: column h*F+f)
+//       [HF, s_off)    zero pad, s_off = round_up(HF, 4)
+//       [s_off, +H)    s_src[h] = Wh_h . a1_h + c1_h
+//       [s_off+H, ld)  zero pad, ld = s_off + round_up(H, 4)
+//   s_dst[n_nodes][H] fp32 (target term, read once per row)
+//   CSR by target: rowptr int32 [n+1], col int32 [E+n]; within a row the
+//   input edge order is kept (stable sort) and the self-loop is last,
+//   exactly the order add_self_loops produces.
+//
+// Everything is fp32 (parity bar 1e-5 vs the reference's fp32 CPU path).
+// No CUDA shims, no hipify, no multi-backend code: gfx950 only.
+
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <cmath>
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/gat_amd.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float leaky(float z, float slope) {
+    // torch.nn.LeakyReLU: z > 0 ? z : z * slope
+    return z > 0.f ? z : z * slope;
+}
+
+__host__ __device__ constexpr int round_up4(int v) { return (v + 3) & ~3; }
+
+int next_pow2(int v) {
+    int p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+// ---------------------------------------------------------------------------
+// Projection: T[:, :HF] = X W^T + b, s_src / s_dst fused in the epilogue.
+//
+// One 256-thread workgroup (4 waves) owns BM = 64 node rows and ALL HF output
+// columns (so each head's score dot product stays in the workgroup).  Each
+// wave owns 16 rows x (NT * 16) columns as NT accumulators of
+// v_mfma_f32_16x16x4_f32 (exact fp32, k-ordered fma chain).  X and W tiles
+// are staged through LDS, BK = 32 deep.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void k_project(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ T, int ld, int s_off,
+    float* __restrict__ s_dst) {
+    constexpr int BM = 64, BK = 32, BN = NT * 16;
+    constexpr int XS = BK + 2;  // 2-float pad: the 16x16x4 A/B reads are conflict-free
+    constexpr int OS = BN + 1;
+    constexpr int MAIN = (BM + BN) * XS;
+    constexpr int EPIL = BM * OS;
+    __shared__ float smem[MAIN > EPIL ? MAIN : EPIL];
+    float* Xs = smem;
+    float* Ws = smem + BM * XS;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int row0 = blockIdx.x * BM;
+
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int k0 = 0; k0 < fin; k0 += BK) {
+        for (int idx = tid; idx < BM * BK; idx += 256) {
+            const int rr = idx / BK, kk = idx % BK;
+            const int gr = row0 + rr, gk = k0 + kk;
+            Xs[rr * XS + kk] = (gr < n && gk < fin) ? X[(size_t)gr * fin + gk] : 0.f;
+        }
+        for (int idx = tid; idx < BN * BK; idx += 256) {
+            const int nn = idx / BK, kk = idx % BK;
+            const int gk = k0 + kk;
+            Ws[nn * XS + kk] = (nn < HF && gk < fin) ? W[(size_t)nn * fin + gk] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < BK; ks += 4) {
+            // 16x16x4 f32 operand maps: A[l&15][k=l>>4], B[k=l>>4][l&15]
+            const float a = Xs[(w * 16 + (lane & 15)) * XS + ks + (lane >> 4)];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float b = Ws[(t * 16 + (lane & 15)) * XS + ks + (lane >> 4)];
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+
+    // C/D map: col = lane & 15, row = (lane >> 4) * 4 + i
+    float* Os = smem;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            Os[(w * 16 + (lane >> 4) * 4 + i) * OS + t * 16 + (lane & 15)] = acc[t][i];
+    __syncthreads();
+    // + Linear bias b_h (inside Wh, GAT.py:43)
+    for (int idx = tid; idx < BM * HF; idx += 256) {
+        const int rr = idx / HF, cc = idx % HF;
+        Os[rr * OS + cc] += bW[cc];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < BM * s_off; idx += 256) {
+        const int rr = idx / s_off, cc = idx % s_off;
+        const int gr = row0 + rr;
+        if (gr < n) T[(size_t)gr * ld + cc] = cc < HF ? Os[rr * OS + cc] : 0.f;
+    }
+    // attention Linears on the fp32 Wh (GAT.py:44-45): s = Wh_h . a_h + c_h
+    const int sw = ld - s_off;
+    for (int idx = tid; idx < BM * sw; idx += 256) {
+        const int rr = idx / sw, h = idx % sw;
+        const int gr = row0 + rr;
+        if (gr >= n) continue;
+        float s1 = 0.f, s2 = 0.f;
+        if (h < H) {
+            for (int f = 0; f < F; ++f) {
+                const float v = Os[rr * OS + h * F + f];
+                s1 = fmaf(v, a1[h * F + f], s1);
+                s2 = fmaf(v, a2[h * F + f], s2);
+            }
+            s1 += c1[h];
+            s2 += c2[h];
+            s_dst[(size_t)gr * H + h] = s2;
+        }
+        T[(size_t)gr * ld + s_off + h] = s1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Edge kernel: one wavefront (= one 64-thread workgroup) per target row.
+//
+// For each chunk of C in-edges of row r:
+//   score phase  lane (k, h) slots: e = LeakyReLU(s_dst[r,h] + s_src[col_k,h]),
+//                chunk max per head by xor-shuffle, online rescale of (m, l),
+//                p = exp(e - m) staged in LDS.
+//   gather phase LPE lanes per edge, each a float4 of the source's Wh row
+//                (one 256 B coalesced row read per edge at HF = 64),
+//                acc += p[head] * Wh.  U steps in flight per lane.
+// Row end: acc reduced across edge slots, divided by (l + 1e-16) (PyG
+// softmax's epsilon), concat -> +bias, mean -> head mean via LDS, +bias.
+// Optional lse[r,h] = m + log(l) for the backward pass.
+// ---------------------------------------------------------------------------
+template <int LPE, int HP>
+__global__ __launch_bounds__(64) void k_edge_fwd(
+    const int* __restrict__ rowptr, const int* __restrict__ col, int row_begin, int row_end,
+    const float* __restrict__ T, int ld, int s_off, const float* __restrict__ s_dst,
+    int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
+    float* __restrict__ out, int ld_out, float* __restrict__ lse) {
+    constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;  // edges per chunk
+    constexpr int R = C * HP / kWave;                          // score slots per lane
+    constexpr int EPI = kWave / LPE;                           // edges per gather step
+    constexpr int U = (EPI >= 16) ? 2 : 4;                     // gather steps in flight
+    __shared__ int col_s[C];
+    __shared__ float p_s[C * HP];
+    __shared__ float hv_s[HP];
+    __shared__ float y_s[LPE * 4];
+
+    const int lane = threadIdx.x;
+    const int r = row_begin + blockIdx.x;
+    if (r >= row_end) return;
+    const int e0 = rowptr[r], e1 = rowptr[r + 1];
+
+    const int hs = lane & (HP - 1);
+    const bool hs_ok = hs < H;
+    const float sd = hs_ok ? s_dst[(size_t)r * H + hs] : 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    const int c = lane & (LPE - 1);
+    const int slot = lane / LPE;
+    const bool c_ok = 4 * c < HF;
+    const int coff = c_ok ? 4 * c : 0;
+    int hq[4];
+    bool cq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int f = 4 * c + q;
+        cq[q] = f < HF;
+        hq[q] = cq[q] ? f / F : 0;
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+
+    for (int base = e0; base < e1; base += C) {
+        const int nk = min(C, e1 - base);
+        if (lane < nk) col_s[lane] = col[base + lane];
+        __syncthreads();
+
+        float ev[R];
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int k = (lane + kWave * q) / HP;
+            float e = -INFINITY;
+            if (k < nk && hs_ok) {
+                const int j = col_s[k];
+                e = leaky(sd + T[(size_t)j * ld + s_off + hs], slope);
+            }
+            ev[q] = e;
+            mloc = fmaxf(mloc, e);
+        }
+#pragma unroll
+        for (int off = HP; off < kWave; off <<= 1) mloc = fmaxf(mloc, __shfl_xor(mloc, off));
+        const float m_new = fmaxf(m_run, mloc);
+        const float scale = hs_ok ? expf(m_run - m_new) : 1.f;
+        l_run *= scale;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const float p = (ev[q] == -INFINITY) ? 0.f : expf(ev[q] - m_new);
+            l_run += p;
+            p_s[lane + kWave * q] = p;
+        }
+        if (lane < HP) hv_s[lane] = scale;
+        m_run = m_new;
+        __syncthreads();
+
+        acc.x *= hv_s[hq[0]];
+        acc.y *= hv_s[hq[1]];
+        acc.z *= hv_s[hq[2]];
+        acc.w *= hv_s[hq[3]];
+
+        for (int k0 = 0; k0 < nk; k0 += EPI * U) {
+            f32x4 v[U];
+            f32x4 pv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = k0 + u * EPI + slot;
+                const bool ok = k < nk;
+                const int kk = ok ? k : nk - 1;
+                const int j = col_s[kk];
+                v[u] = *reinterpret_cast<const f32x4*>(T + (size_t)j * ld + coff);
+                const float* pr = p_s + kk * HP;
+                const float g = ok ? 1.f : 0.f;
+                pv[u] = f32x4{pr[hq[0]] * g, pr[hq[1]] * g, pr[hq[2]] * g, pr[hq[3]] * g};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += pv[u] * v[u];
+        }
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int off = HP; off < kWave; off <<= 1) l_run += __shfl_xor(l_run, off);
+#pragma unroll
+    for (int off = LPE; off < kWave; off <<= 1) {
+        acc.x += __shfl_xor(acc.x, off);
+        acc.y += __shfl_xor(acc.y, off);
+        acc.z += __shfl_xor(acc.z, off);
+        acc.w += __shfl_xor(acc.w, off);
+    }
+    if (lane < HP) hv_s[lane] = 1.f / (l_run + 1e-16f);
+    if (lse != nullptr && lane < H) lse[(size_t)r * H + lane] = m_run + logf(l_run);
+    __syncthreads();
+    float y[4] = {acc.x * hv_s[hq[0]], acc.y * hv_s[hq[1]], acc.z * hv_s[hq[2]],
+                  acc.w * hv_s[hq[3]]};
+    if (concat) {
+        if (slot == 0 && c_ok) {
+            float* o = out + (size_t)r * ld_out + 4 * c;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (cq[q]) o[q] = y[q] + bias[4 * c + q];
+        }
+    } else {
+        if (slot == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (cq[q]) y_s[4 * c + q] = y[q];
+        }
+        __syncthreads();
+        for (int f = lane; f < F; f += kWave) {
+            float s = 0.f;
+            for (int h = 0; h < H; ++h) s += y_s[h * F + f];
+            out[(size_t)r * ld_out + f] = s / (float)H + bias[f];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CSR-by-target build with appended self-loops.
+// ---------------------------------------------------------------------------
+__global__ void k_csr_prepare(const long long* __restrict__ ei, long long E, int n,
+                              unsigned* __restrict__ keys, int* __restrict__ vals,
+                              int* __restrict__ err) {
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < E;
+         k += (long long)gridDim.x * blockDim.x) {
+        const long long s = ei[k], d = ei[E + k];
+        const bool ok = s >= 0 && s < n && d >= 0 && d < n;
+        if (!ok) atomicOr(err, 1);
+        keys[k] = ok ? (unsigned)d : 0u;
+        vals[k] = ok ? (int)s : 0;
+    }
+}
+
+__global__ void k_csr_rowptr(const unsigned* __restrict__ sorted_keys, long long E, int n,
+                             int* __restrict__ rowptr) {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (i > n) return;
+    // lower_bound(sorted_keys, i): edges with target < i, plus one loop per earlier row
+    long long lo = 0, hi = E;
+    while (lo < hi) {
+        const long long mid = (lo + hi) >> 1;
+        if (sorted_keys[mid] < (unsigned)i) lo = mid + 1; else hi = mid;
+    }
+    rowptr[i] = (int)(lo + i);
+}
+
+__global__ void k_csr_scatter(const unsigned* __restrict__ sorted_keys,
+                              const int* __restrict__ sorted_vals, long long E, int n,
+                              const int* __restrict__ rowptr, int* __restrict__ col) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long s = blockIdx.x * (long long)blockDim.x + threadIdx.x; s < E; s += stride)
+        col[s + sorted_keys[s]] = sorted_vals[s];
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+        col[rowptr[i + 1] - 1] = (int)i;  // the appended self-loop closes each row
+}
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
+
+unsigned key_bits(int n) {
+    unsigned b = 1;
+    while (b < 31 && (1u << b) < (unsigned)n) ++b;
+    return b;
+}
+
+size_t radix_tmp_bytes(long long E, int n) {
+    size_t tmp = 0;
+    unsigned* k = nullptr;
+    int* v = nullptr;
+    const hipError_t e = rocprim::radix_sort_pairs(nullptr, tmp, k, k, v, v, (size_t)E, 0u, key_bits(n));
+    return e == hipSuccess ? tmp : 0;
+}
+
+inline int grid_for(long long work, int block, int cap = 256 * 16) {
+    long long g = (work + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+int status_of(hipError_t e) { return e == hipSuccess ? GAT_OK : (int)e; }
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int gat_abi_version(void) { return GAT_ABI_VERSION; }
+
+int gat_table_layout(int heads, int f, int* ld, int* s_off) {
+    if (heads <= 0 || f <= 0 || ld == nullptr || s_off == nullptr) return GAT_EINVAL;
+    const int hf = heads * f;
+    *s_off = round_up4(hf);
+    *ld = *s_off + round_up4(heads);
+    return GAT_OK;
+}
+
+int gat_project(const float* x, int n, int fin, const float* w, const float* b,
+                const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,
+                int heads, int f, float* table, int ld, int s_off, float* s_dst, void* stream) {
+    if (n < 0 || fin < 0 || heads <= 0 || f <= 0) return GAT_EINVAL;
+    const int hf = heads * f;
+    if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
+    if (s_off < hf || (s_off & 3) || ld < s_off + heads || (ld & 3)) return GAT_EINVAL;
+    if (n == 0) return GAT_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((n + 63) / 64), block(256);
+    const int nt = (hf + 15) / 16;
+#define GAT_PROJ_CASE(NT)                                                                   \
+    case NT:                                                                                \
+        hipLaunchKernelGGL(k_project<NT>, grid, block, 0, st, x, n, fin, w, b, a_src, c_src, \
+                           a_dst, c_dst, heads, f, hf, table, ld, s_off, s_dst);            \
+        break;
+    switch (nt) {
+        GAT_PROJ_CASE(1) GAT_PROJ_CASE(2) GAT_PROJ_CASE(3) GAT_PROJ_CASE(4)
+        GAT_PROJ_CASE(5) GAT_PROJ_CASE(6) GAT_PROJ_CASE(7) GAT_PROJ_CASE(8)
+        GAT_PROJ_CASE(9) GAT_PROJ_CASE(10) GAT_PROJ_CASE(11) GAT_PROJ_CASE(12)
+        GAT_PROJ_CASE(13) GAT_PROJ_CASE(14) GAT_PROJ_CASE(15) GAT_PROJ_CASE(16)
+        default: return GAT_EUNSUPPORTED;
+    }
+#undef GAT_PROJ_CASE
+    return status_of(hipGetLastError());
+}
+
+int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row_end,
+                       const float* table, int ld, int s_off, const float* s_dst, int heads,
+                       int f, int concat, float negative_slope, const float* bias, float* out,
+                       float* lse, void* stream) {
+    if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
+    const int hf = heads * f;
+    if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
+    if (s_off < hf || (s_off & 3) || ld < s_off + heads || (ld & 3)) return GAT_EINVAL;
+    const int rows = row_end - row_begin;
+    if (rows == 0) return GAT_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const int lpe = next_pow2((round_up4(hf) + 3) / 4);
+    const int hp = next_pow2(heads);
+    const int ld_out = concat ? hf : f;
+    const dim3 grid(rows), block(kWave);
+#define GAT_EDGE_LAUNCH(L, P)                                                                \
+    hipLaunchKernelGGL((k_edge_fwd<L, P>), grid, block, 0, st, rowptr, col, row_begin,       \
+                       row_end, table, ld, s_off, s_dst, heads, f, hf, concat,              \
+                       negative_slope, bias, out, ld_out, lse)
+#define GAT_EDGE_HP(L)                                                                       \
+    switch (hp) {                                                                            \
+        case 1: GAT_EDGE_LAUNCH(L, 1); break;                                                \
+        case 2: GAT_EDGE_LAUNCH(L, 2); break;                                                \
+        case 4: GAT_EDGE_LAUNCH(L, 4); break;                                                \
+        case 8: GAT_EDGE_LAUNCH(L, 8); break;                                                \
+        case 16: GAT_EDGE_LAUNCH(L, 16); break;                                              \
+        case 32: GAT_EDGE_LAUNCH(L, 32); break;                                              \
+        case 64: GAT_EDGE_LAUNCH(L, 64); break;                                              \
+        default: return GAT_EUNSUPPORTED;                                                    \
+    }
+    switch (lpe) {
+        case 1: GAT_EDGE_HP(1) break;
+        case 2: GAT_EDGE_HP(2) break;
+        case 4: GAT_EDGE_HP(4) break;
+        case 8: GAT_EDGE_HP(8) break;
+        case 16: GAT_EDGE_HP(16) break;
+        case 32: GAT_EDGE_HP(32) break;
+        case 64: GAT_EDGE_HP(64) break;
+        default: return GAT_EUNSUPPORTED;
+    }
+#undef GAT_EDGE_HP
+#undef GAT_EDGE_LAUNCH
+    return status_of(hipGetLastError());
+}
+
+int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes) {
+    if (num_edges < 0 || num_nodes < 0 || bytes == nullptr) return GAT_EINVAL;
+    if (num_edges + num_nodes > 0x7fffffffLL) return GAT_EUNSUPPORTED;
+    const size_t e = (size_t)(num_edges > 0 ? num_edges : 1);
+    *bytes = 4 * align_up(e * 4) + align_up(radix_tmp_bytes(num_edges, num_nodes > 0 ? num_nodes : 1));
+    return GAT_OK;
+}
+
+int gat_csr_build(const long long* edge_index, long long num_edges, int num_nodes, int* rowptr,
+                  int* col, void* workspace, size_t workspace_bytes, int* error_flag,
+                  void* stream) {
+    if (num_edges < 0 || num_nodes < 0 || error_flag == nullptr) return GAT_EINVAL;
+    size_t need = 0;
+    int rc = gat_csr_workspace_size(num_edges, num_nodes, &need);
+    if (rc != GAT_OK) return rc;
+    if (workspace_bytes < need) return GAT_EWORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(error_flag, 0, sizeof(int), st);
+    if (e != hipSuccess) return status_of(e);
+    if (num_nodes == 0) {
+        if (num_edges > 0) {
+            // every edge is out of range when there are no nodes
+            e = hipMemsetAsync(error_flag, 0x01, 1, st);
+            if (e != hipSuccess) return status_of(e);
+        }
+        return status_of(hipMemsetAsync(rowptr, 0, sizeof(int), st));
+    }
+    const long long E = num_edges;
+    const size_t eb = align_up((size_t)(E > 0 ? E : 1) * 4);
+    char* ws = (char*)workspace;
+    unsigned* keys_in = (unsigned*)(ws);
+    int* vals_in = (int*)(ws + eb);
+    unsigned* keys_out = (unsigned*)(ws + 2 * eb);
+    int* vals_out = (int*)(ws + 3 * eb);
+    void* tmp = ws + 4 * eb;
+    if (E > 0) {
+        hipLaunchKernelGGL(k_csr_prepare, dim3(grid_for(E, 256)), dim3(256), 0, st, edge_index,
+                           E, num_nodes, keys_in, vals_in, error_flag);
+        size_t tmp_bytes = need - 4 * eb;
+        e = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out,
+                                      (size_t)E, 0u, key_bits(num_nodes), st);
+        if (e != hipSuccess) return status_of(e);
+    }
+    hipLaunchKernelGGL(k_csr_rowptr, dim3((num_nodes + 1 + 255) / 256), dim3(256), 0, st,
+                       keys_out, E, num_nodes, rowptr);
+    hipLaunchKernelGGL(k_csr_scatter, dim3(grid_for(E > num_nodes ? E : num_nodes, 256)),
+                       dim3(256), 0, st, keys_out, vals_out, E, num_nodes, rowptr, col);
+    return status_of(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: edges/sec through the 8-head GAT layer forward, PPI shape.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ppi|reddit|arxiv|cifar...]
+
+A "step" is one GraphAttentionLayer forward (eval, fp32) over the synthetic
+PPI-shape graph (BASELINE.json configs[1]: N=44,906, E=1,226,368 + N loops,
+Fin=50, H=8, F=8, concat) with inputs resident in HBM: the HIP projection +
+the fused edge kernel.  The CSR (built once per edge_index and cached, as in
+the module) is outside the timed region; it is timed separately.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+METRIC = "edges/sec through 8-head GAT layer forward, PPI shape, at 1/2/4/8 MI355X"
+
+
+def edge_kernel_bytes(n_rows: int, n_edges: int, heads: int, f: int, concat: bool) -> int:
+    """Algorithmic HBM bytes of one edge-kernel launch:
+    per edge 4 (col) + 4*H*F (Wh_j) + 4*H (s_src_j); per target row
+    4 (rowptr) + 4*H (s_dst) + 4*C_out (output write)."""
+    c_out = heads * f if concat else f
+    return n_edges * (4 + 4 * heads * f + 4 * heads) + n_rows * (4 + 4 * heads + 4 * c_out)
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def load_traffic(workload: str):
+    """Per-launch HBM bytes of the edge kernel from the committed PMC summary
+    (tools/pmc_traffic.py -> profiles/pmc_<workload>.json), if present."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get("edge_kernel_hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(layer_state, x, ei, heads, concat, n_edges_total, budget_s: float = 12.0):
+    """The oracle (pure-PyTorch restatement of GAT.py:37-67, same op order)
+    on the host cores over the same synthetic workload; bounded to ~budget_s."""
+    from oracle import gat_layer_forward_from_state
+
+    threads = torch.get_num_threads()
+    xc, eic = x.cpu(), ei.cpu()
+    st = {k: v.cpu() for k, v in layer_state.items()}
+    gat_layer_forward_from_state(st, xc, eic, heads, concat)  # warm-up
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 5 and (time.perf_counter() - t_start) < budget_s:
+        t0 = time.perf_counter()
+        gat_layer_forward_from_state(st, xc, eic, heads, concat)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": n_edges_total / med, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": (f"full workload, {len(times)} timed fwd after 1 warm-up, median "
+                       f"{med * 1e3:.1f} ms; oracle/gat_oracle.py (torch CPU, "
+                       f"{threads} threads, {cpu_model()})")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="ppi")
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of a HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--edge-iters", type=int, default=50)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if world > 1 or args.gpus > 1:
+        from atmlgraphattentionnetworks_amd.distributed import bench_distributed
+        return bench_distributed(args, METRIC)
+
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
+    from atmlgraphattentionnetworks_amd.layer import edge_aggregate, project
+    from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
+
+    dev = torch.device("cuda", 0)
+    w = WORKLOADS[args.workload]
+    x, ei = make_inputs(w, dev)
+    n = x.size(0)
+    torch.manual_seed(0)
+    layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
+                                concat=w.concat).to(dev).eval()
+
+    # CSR build (one-time, cached by the module): timed separately
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    csr = get_csr(ei, n)
+    torch.cuda.synchronize()
+    csr_ms = (time.perf_counter() - t0) * 1e3
+    n_edges = csr.num_edges
+
+    def step():
+        return layer(x, ei)
+
+    with torch.no_grad():
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        graph = None
+        if not args.no_graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                static_out = step()
+            run = graph.replay
+        else:
+            run = step
+        for _ in range(args.warmup):
+            run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ms_per_step = elapsed * 1e3 / args.steps
+
+        # edge kernel alone, HIP events on the stream it is launched on
+        pp = layer.packed()
+        table, s_dst = project(x, pp, w.heads, w.out_channels)
+        out = torch.empty(n, w.heads * w.out_channels if w.concat else w.out_channels,
+                          device=dev)
+        for _ in range(5):
+            edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat, layer.bias,
+                           out=out)
+        stream = torch.cuda.current_stream()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(args.edge_iters):
+            edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat, layer.bias,
+                           out=out)
+        ev1.record(stream)
+        ev1.synchronize()
+        edge_ms = ev0.elapsed_time(ev1) / args.edge_iters
+        # projection alone
+        ev0.record(stream)
+        for _ in range(args.edge_iters):
+            project(x, pp, w.heads, w.out_channels, table=table, s_dst=s_dst)
+        ev1.record(stream)
+        ev1.synchronize()
+        proj_ms = ev0.elapsed_time(ev1) / args.edge_iters
+
+    alg_bytes = edge_kernel_bytes(n, n_edges, w.heads, w.out_channels, w.concat)
+    achieved = alg_bytes / (edge_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.workload)
+    result = {
+        "metric": METRIC,
+        "value": n_edges / (ms_per_step * 1e-3),
+        "unit": "edges/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded uniform graph of the PPI shape; reference-order random init)",
+        "config": {"workload": f"{w.name}: N={n} E={w.num_edges if w.kind == 'uniform' else ei.size(1)}"
+                               f" (+N self-loops = {n_edges}) Fin={w.in_channels} H={w.heads}"
+                               f" F={w.out_channels} concat={w.concat}",
+                   "parallelism": "single GPU", "launch": "hipGraph" if graph else "eager"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_edge_fwd", "kernel_ms": edge_ms,
+                     "algorithmic_bytes_per_launch": alg_bytes},
+        "breakdown_ms": {"project": proj_ms, "edge": edge_ms, "csr_build_once": csr_ms},
+    }
+    if not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(layer.state_dict(), x, ei, w.heads, w.concat,
+                                              n_edges)
+    print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,110 @@
+/*
+ * gat_amd.h — C-ABI of the MI355X (gfx950) GAT attention-layer library
+ * (libgat_amd.so, built from atmlgraphattentionnetworks_amd/csrc/gat_amd.hip).
+ *
+ * Drop-in boundary for the hot path of danieldritter/ATMLGraphAttentionNetworks:
+ * GraphAttentionLayer.forward(x, edge_index), GAT.py:37-67, and the PyG calls it
+ * makes.  The reference is pure Python (it has no FFI of its own); the host side
+ * above this ABI is the Python module atmlgraphattentionnetworks_amd.GraphAttentionLayer,
+ * which keeps the reference's constructor, attributes and state_dict, and binds
+ * these symbols with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer owned by the caller; the library never
+ *    allocates or frees (CSR build takes a caller workspace sized by
+ *    gat_csr_workspace_size).
+ *  - `stream` is a hipStream_t passed as void* (torch's current stream).
+ *    All work is enqueued on it; nothing synchronises the host.
+ *  - Return value: GAT_OK (0), a negative GAT_E* code for bad arguments, or a
+ *    positive hipError_t from the launch.  No exceptions cross the ABI.
+ *  - Stateless and reentrant; safe to call concurrently on different devices
+ *    or streams.
+ *  - fp32 everywhere for features; int32 CSR indices; int64 edge_index input
+ *    (the reference's LongTensor).
+ */
+#ifndef GAT_AMD_H_
+#define GAT_AMD_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GAT_ABI_VERSION 1
+
+#define GAT_OK 0
+#define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
+#define GAT_EUNSUPPORTED (-2) /* shape outside the kernels' range (see limits)    */
+#define GAT_EWORKSPACE (-3)   /* workspace smaller than gat_csr_workspace_size      */
+
+#define GAT_MAX_HEADS 64 /* num_heads                    */
+#define GAT_MAX_HF 256   /* num_heads * output_channels  */
+
+/* ABI version of the loaded library (== GAT_ABI_VERSION). */
+int gat_abi_version(void);
+
+/*
+ * Node-table layout for (heads, f): row stride `ld` floats and the column
+ * `s_off` where s_src starts.  Row n = [Wh[n] (heads*f) | 0-pad | s_src[n] (heads) | 0-pad],
+ * both parts 16-byte aligned.  Wh is head-major (column h*f + k), i.e. the
+ * reference's stack/transpose [N,H,F] view (GAT.py:49-50) made contiguous.
+ */
+int gat_table_layout(int heads, int f, int* ld, int* s_off);
+
+/*
+ * Dense head projection with fused attention scores.
+ * Replaces GAT.py:42-52 (per head h: ws[h](x), attentions1[h](.), attentions2[h](.),
+ * then stack/transpose).
+ *   x      [n, fin]      row-major
+ *   w      [heads*f, fin] = cat_h ws[h].weight          (GAT.py:20)
+ *   b      [heads*f]      = cat_h ws[h].bias
+ *   a_src  [heads*f]      = cat_h attentions1[h].weight  (GAT.py:21, source term)
+ *   c_src  [heads]        = cat_h attentions1[h].bias
+ *   a_dst, c_dst          = the same for attentions2     (GAT.py:22, target term)
+ * Writes table rows [0, n) (layout above) and s_dst [n, heads].
+ */
+int gat_project(const float* x, int n, int fin, const float* w, const float* b,
+                const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,
+                int heads, int f, float* table, int ld, int s_off, float* s_dst, void* stream);
+
+/*
+ * Fused per-edge score + LeakyReLU + segmented softmax + attention-weighted
+ * aggregation + concat/head-mean + bias over target rows [row_begin, row_end).
+ * Replaces GAT.py:53-67 (PyG propagate/__collect__, message, utils.softmax,
+ * aggregate aggr='add') and GAT.py:54 (+ bias).
+ *   rowptr/col  CSR by target (gat_csr_build); col holds table row ids
+ *   table       node table (gat_project / an all-gathered copy)
+ *   s_dst       [rows, heads], indexed by target row
+ *   bias        [heads*f] if concat else [f]
+ *   out         [rows, heads*f] if concat else [rows, f], indexed by target row
+ *   lse         optional [rows, heads] = max + log(sum exp) per (row, head)
+ *               (for the backward pass); may be NULL
+ */
+int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row_end,
+                       const float* table, int ld, int s_off, const float* s_dst, int heads,
+                       int f, int concat, float negative_slope, const float* bias, float* out,
+                       float* lse, void* stream);
+
+/* Workspace bytes gat_csr_build needs for (num_edges, num_nodes). */
+int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);
+
+/*
+ * COO -> CSR by target with the N self-loops appended.
+ * Replaces torch_geometric.utils.add_self_loops (GAT.py:38) and the grouping of
+ * edges by edge_index[1] that PyG's propagate/softmax/scatter perform (GAT.py:53,60).
+ *   edge_index [2, num_edges] int64 (row 0 = source, row 1 = target)
+ *   rowptr     [num_nodes + 1] int32,  col [num_edges + num_nodes] int32
+ * Within a row the input edge order is kept and the loop comes last, matching
+ * cat([edge_index, loops]).  Existing self-loops and multi-edges are kept.
+ * *error_flag (device int) is set non-zero if any index is outside [0, num_nodes).
+ */
+int gat_csr_build(const long long* edge_index, long long num_edges, int num_nodes, int* rowptr,
+                  int* col, void* workspace, size_t workspace_bytes, int* error_flag,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GAT_AMD_H_ */

@@ -1,0 +1,52 @@
+"""The oracle (oracle/gat_oracle.py) against the golden vectors produced by
+the reference's own GAT.py (tests/golden/make_golden.py), and against the
+float64 closed form on the known-answer graphs.  CPU only."""
+import pytest
+import torch
+
+from conftest import golden_names, load_golden
+from oracle import closed_form_forward, gat_layer_forward_from_state, init_reference_params
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_oracle_matches_reference_fixture(name):
+    g = load_golden(name)
+    m = g["meta"]
+    out = gat_layer_forward_from_state(g["state"], g["x"], g["edge_index"], m["H"], m["concat"])
+    assert out.shape == g["out"].shape
+    # same op sequence on the same CPU -> bit-identical
+    assert torch.equal(out, g["out"])
+
+
+@pytest.mark.parametrize("name", [n for n in golden_names() if n.startswith("kat_")])
+def test_known_answer_closed_form(name):
+    g = load_golden(name)
+    m = g["meta"]
+    cf = closed_form_forward(g["state"], g["x"], g["edge_index"], m["H"], m["concat"])
+    torch.testing.assert_close(g["out"].double(), cf, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_reference_init_order(name):
+    """init_reference_params reproduces the reference constructor's RNG order."""
+    g = load_golden(name)
+    m = g["meta"]
+    st = init_reference_params(m["Fin"], m["F"], m["H"], m["concat"], seed=m["seed"])
+    assert list(st.keys()) == list(g["state"].keys())
+    for k in st:
+        assert torch.equal(st[k], g["state"][k]), k
+
+
+def test_src_dst_convention():
+    """attentions1 is the SOURCE term, attentions2 the TARGET term: swapping
+    them changes the result on an asymmetric graph."""
+    g = load_golden("kat_asym3")
+    m = g["meta"]
+    st = dict(g["state"])
+    for h in range(m["H"]):
+        st[f"attentions1.{h}.weight"], st[f"attentions2.{h}.weight"] = (
+            st[f"attentions2.{h}.weight"], st[f"attentions1.{h}.weight"])
+        st[f"attentions1.{h}.bias"], st[f"attentions2.{h}.bias"] = (
+            st[f"attentions2.{h}.bias"], st[f"attentions1.{h}.bias"])
+    swapped = gat_layer_forward_from_state(st, g["x"], g["edge_index"], m["H"], m["concat"])
+    assert not torch.allclose(swapped, g["out"], atol=1e-4)
