@@ -30,6 +30,8 @@
 #include <cmath>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 
 #include "../../include/gat_amd.h"
 
@@ -298,6 +300,244 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 }
 
 // ---------------------------------------------------------------------------
+// Projection, register-direct variant (F divides 16 or F % 16 == 0).
+//
+// Each wave owns 16 node rows x all NT*16 columns.  MFMA A/B fragments are
+// loaded straight from global memory (W is a few KB and stays in L1/L2; each
+// X row is read once), so the kernel has no LDS and no barriers.  The
+// epilogue works on the accumulators in place: bias add, Wh stores, and the
+// two attention dot products reduced across the F lanes of each head with
+// xor-shuffles (F | 16) or across whole tiles then 16 lanes (F % 16 == 0).
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void k_project_reg(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ T, int ld, int s_off,
+    float* __restrict__ s_dst) {
+    constexpr int KU = 4;  // k-steps (of 4) per unrolled block
+    const int lane = threadIdx.x & 63;
+    const int row0 = (blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6)) * 16;
+    if (row0 >= n) return;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int ar = row0 + cl;
+    const float* xr = X + (size_t)(ar < n ? ar : n - 1) * fin;
+    const float xs = ar < n ? 1.f : 0.f;
+    const float* wr[NT];
+    float ws[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int cc = t * 16 + cl;
+        wr[t] = W + (size_t)(cc < HF ? cc : 0) * fin;
+        ws[t] = cc < HF ? 1.f : 0.f;
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int k = 0;
+    for (; k + 4 * KU <= fin; k += 4 * KU) {
+        float a[KU], b[KU][NT];
+#pragma unroll
+        for (int u = 0; u < KU; ++u) {
+            a[u] = xr[k + 4 * u + kq] * xs;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) b[u][t] = wr[t][k + 4 * u + kq] * ws[t];
+        }
+#pragma unroll
+        for (int u = 0; u < KU; ++u)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u][t], acc[t], 0, 0, 0);
+    }
+    for (; k < fin; k += 4) {
+        const int kk = k + kq;
+        const bool ok = kk < fin;
+        const float a = ok ? xr[kk] * xs : 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const float b = ok ? wr[t][kk] * ws[t] : 0.f;
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+        }
+    }
+
+    // accumulator map: column t*16 + cl, rows (lane >> 4) * 4 + i
+    float s1[NT][4], s2[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int cc = t * 16 + cl;
+        const bool cv = cc < HF;
+        const float bb = cv ? bW[cc] : 0.f;
+        const float w1 = cv ? a1[cc] : 0.f, w2 = cv ? a2[cc] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float v = acc[t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
+            acc[t][i] = v;
+            s1[t][i] = v * w1;
+            s2[t][i] = v * w2;
+            const int rr = row0 + (lane >> 4) * 4 + i;
+            if (rr < n && cc < s_off) T[(size_t)rr * ld + cc] = v;
+        }
+    }
+    if (F <= 16) {
+        // head = F consecutive lanes of one tile
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                for (int off = 1; off < F; off <<= 1) {
+                    s1[t][i] += __shfl_xor(s1[t][i], off);
+                    s2[t][i] += __shfl_xor(s2[t][i], off);
+                }
+        if ((cl & (F - 1)) == 0) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int h = (t * 16 + cl) / F;
+                if (h >= H) continue;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = row0 + (lane >> 4) * 4 + i;
+                    if (rr >= n) continue;
+                    T[(size_t)rr * ld + s_off + h] = s1[t][i] + c1[h];
+                    s_dst[(size_t)rr * H + h] = s2[t][i] + c2[h];
+                }
+            }
+        }
+    } else {
+        // F % 16 == 0: head h spans tiles [h*F/16, (h+1)*F/16)
+        const int tph = F / 16;
+        for (int h = 0; h < H; ++h) {
+            float p1[4] = {0.f, 0.f, 0.f, 0.f}, p2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                if (t / tph != h) continue;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    p1[i] += s1[t][i];
+                    p2[i] += s2[t][i];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                for (int off = 1; off < 16; off <<= 1) {
+                    p1[i] += __shfl_xor(p1[i], off);
+                    p2[i] += __shfl_xor(p2[i], off);
+                }
+            if (cl == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = row0 + (lane >> 4) * 4 + i;
+                    if (rr >= n) continue;
+                    T[(size_t)rr * ld + s_off + h] = p1[i] + c1[h];
+                    s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Edge kernel, lane-group variant (F % 4 == 0): G = next_pow2(HF/4) lanes per
+// target row, 64/G rows per wave, one row per group.
+//
+// Lane c of a group owns the float4 columns [4c, 4c+4) of the row — all in
+// head h = 4c / F — and runs that head's online softmax in registers, so the
+// hot loop has no LDS traffic, no barriers and no cross-lane reductions.
+// Per chunk of U in-edges: one coalesced col load, U broadcasts by shuffle,
+// then U independent (s_src, Wh float4) gathers in flight per lane, one
+// rescale per chunk.  Head mean (concat=False, F/4 a power of two) is an
+// xor-butterfly over the group.
+// ---------------------------------------------------------------------------
+template <int G, int U>
+__global__ __launch_bounds__(256) void k_edge_grp(
+    const int* __restrict__ rowptr, const int* __restrict__ col, int row_begin, int row_end,
+    const float* __restrict__ T, int ld, int s_off, const float* __restrict__ s_dst,
+    int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
+    float* __restrict__ out, int ld_out, float* __restrict__ lse) {
+    constexpr int CL = (U + G - 1) / G;  // col values held per lane per chunk
+    const int lane = threadIdx.x & 63;
+    const int c = lane & (G - 1);
+    const int gbase = lane & ~(G - 1);
+    const int r = row_begin + (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    if (r >= row_end) return;
+    const bool c_ok = 4 * c < HF;
+    const int coff = c_ok ? 4 * c : 0;
+    const int h = coff / F;
+    const int e0 = rowptr[r], e1 = rowptr[r + 1];
+    const float sd = s_dst[(size_t)r * H + h];
+    float m = -INFINITY, l = 0.f;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+
+    for (int k = e0; k < e1; k += U) {
+        const int nk = min(U, e1 - k);
+        int cv[CL];
+#pragma unroll
+        for (int t = 0; t < CL; ++t) {
+            const int idx = c + t * G;
+            cv[t] = idx < nk ? col[k + idx] : -1;
+        }
+        int j[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) j[u] = __shfl(cv[u / G], gbase + (u % G));
+        float s[U];
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t row = (size_t)(j[u] >= 0 ? j[u] : j[0]) * ld;
+            s[u] = T[row + s_off + h];
+            v[u] = *reinterpret_cast<const f32x4*>(T + row + coff);
+        }
+        float emax = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            s[u] = j[u] >= 0 ? leaky(sd + s[u], slope) : -INFINITY;
+            emax = fmaxf(emax, s[u]);
+        }
+        const float m_new = fmaxf(m, emax);
+        const float scale = expf(m - m_new);
+        l *= scale;
+        acc *= scale;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float p = expf(s[u] - m_new);
+            l += p;
+            acc += p * v[u];
+        }
+        m = m_new;
+    }
+
+    const float inv = 1.f / (l + 1e-16f);
+    f32x4 y = acc * inv;
+    if (lse != nullptr && c_ok && (coff % F) == 0) lse[(size_t)r * H + h] = m + logf(l);
+    if (concat) {
+        if (c_ok) {
+            const f32x4 b = *reinterpret_cast<const f32x4*>(bias + coff);
+            *reinterpret_cast<f32x4*>(out + (size_t)r * ld_out + coff) = y + b;
+        }
+    } else {
+        if (!c_ok) y = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int off = G / 2; off >= 1; off >>= 1) {
+            if (off < F / 4) break;
+            y.x += __shfl_xor(y.x, off);
+            y.y += __shfl_xor(y.y, off);
+            y.z += __shfl_xor(y.z, off);
+            y.w += __shfl_xor(y.w, off);
+        }
+        if (4 * c < F) {
+            const float hh = (float)H;
+            float* o = out + (size_t)r * ld_out + 4 * c;
+            o[0] = y.x / hh + bias[4 * c + 0];
+            o[1] = y.y / hh + bias[4 * c + 1];
+            o[2] = y.z / hh + bias[4 * c + 2];
+            o[3] = y.w / hh + bias[4 * c + 3];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // CSR-by-target build with appended self-loops.
 // ---------------------------------------------------------------------------
 __global__ void k_csr_prepare(const long long* __restrict__ ei, long long E, int n,
@@ -362,6 +602,23 @@ inline int grid_for(long long work, int block, int cap = 256 * 16) {
 
 int status_of(hipError_t e) { return e == hipSuccess ? GAT_OK : (int)e; }
 
+// Kernel-choice knobs for A/B measurement (not part of the ABI): the
+// specialised kernel is the default wherever the shape allows it.
+bool kernel_choice(const char* env, const char* fast, const char* slow) {
+    const char* v = std::getenv(env);
+    if (v == nullptr) return true;
+    if (std::strcmp(v, slow) == 0) return false;
+    (void)fast;
+    return true;
+}
+
+int edge_unroll() {
+    const char* v = std::getenv("GAT_EDGE_U");
+    if (v == nullptr) return 8;
+    const int u = std::atoi(v);
+    return (u == 4 || u == 16) ? u : 8;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -390,10 +647,16 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
     const int nt = (hf + 15) / 16;
+    const bool reg_ok = (f <= 16 && 16 % f == 0) || (f % 16 == 0);
+    const bool use_reg = reg_ok && kernel_choice("GAT_PROJ_KERNEL", "reg", "generic");
 #define GAT_PROJ_CASE(NT)                                                                   \
     case NT:                                                                                \
-        hipLaunchKernelGGL(k_project<NT>, grid, block, 0, st, x, n, fin, w, b, a_src, c_src, \
-                           a_dst, c_dst, heads, f, hf, table, ld, s_off, s_dst);            \
+        if (use_reg)                                                                        \
+            hipLaunchKernelGGL(k_project_reg<NT>, grid, block, 0, st, x, n, fin, w, b, a_src, \
+                               c_src, a_dst, c_dst, heads, f, hf, table, ld, s_off, s_dst);  \
+        else                                                                                \
+            hipLaunchKernelGGL(k_project<NT>, grid, block, 0, st, x, n, fin, w, b, a_src,   \
+                               c_src, a_dst, c_dst, heads, f, hf, table, ld, s_off, s_dst);  \
         break;
     switch (nt) {
         GAT_PROJ_CASE(1) GAT_PROJ_CASE(2) GAT_PROJ_CASE(3) GAT_PROJ_CASE(4)
@@ -417,9 +680,38 @@ int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row
     const int rows = row_end - row_begin;
     if (rows == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
+    const int ld_out = concat ? hf : f;
+    const int g = next_pow2((hf + 3) / 4);
+    const bool pow2_f4 = (f % 4 == 0) && next_pow2(f / 4) == f / 4;
+    const bool grp_ok = (f % 4 == 0) && (concat || pow2_f4);
+    if (grp_ok && kernel_choice("GAT_EDGE_KERNEL", "group", "generic")) {
+        const int u = edge_unroll();
+        const long long threads = (long long)rows * g;
+        const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+#define GAT_GRP_LAUNCH(G, UU)                                                                  \
+    hipLaunchKernelGGL((k_edge_grp<G, UU>), grid, block, 0, st, rowptr, col, row_begin,        \
+                       row_end, table, ld, s_off, s_dst, heads, f, hf, concat, negative_slope, \
+                       bias, out, ld_out, lse)
+#define GAT_GRP_U(G)                          \
+    if (u == 4) GAT_GRP_LAUNCH(G, 4);         \
+    else if (u == 16) GAT_GRP_LAUNCH(G, 16);  \
+    else GAT_GRP_LAUNCH(G, 8);
+        switch (g) {
+            case 1: GAT_GRP_U(1) break;
+            case 2: GAT_GRP_U(2) break;
+            case 4: GAT_GRP_U(4) break;
+            case 8: GAT_GRP_U(8) break;
+            case 16: GAT_GRP_U(16) break;
+            case 32: GAT_GRP_U(32) break;
+            case 64: GAT_GRP_U(64) break;
+            default: return GAT_EUNSUPPORTED;
+        }
+#undef GAT_GRP_U
+#undef GAT_GRP_LAUNCH
+        return status_of(hipGetLastError());
+    }
     const int lpe = next_pow2((round_up4(hf) + 3) / 4);
     const int hp = next_pow2(heads);
-    const int ld_out = concat ? hf : f;
     const dim3 grid(rows), block(kWave);
 #define GAT_EDGE_LAUNCH(L, P)                                                                \
     hipLaunchKernelGGL((k_edge_fwd<L, P>), grid, block, 0, st, rowptr, col, row_begin,       \

@@ -22,6 +22,25 @@ def dev():
     return torch.device("cuda", 0)
 
 
+# Every parity case runs on the specialised kernels (the default wherever the
+# shape allows) AND on the generic kernels, selected by the library's env knobs.
+VARIANTS = {
+    "fast": {},
+    "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "generic"},
+    "fast_u4": {"GAT_EDGE_U": "4"},
+    "fast_u16": {"GAT_EDGE_U": "16"},
+}
+
+
+@pytest.fixture(params=list(VARIANTS))
+def variant(request, monkeypatch):
+    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in VARIANTS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
 def layer_from_state(state, fin, F, H, concat):
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer
     layer = GraphAttentionLayer(fin, F, num_heads=H, concat=concat)
@@ -35,7 +54,7 @@ def run_layer(layer, x, ei):
 
 
 @pytest.mark.parametrize("name", golden_names())
-def test_golden_fixture(name):
+def test_golden_fixture(name, variant):
     g = load_golden(name)
     m = g["meta"]
     layer = layer_from_state(g["state"], m["Fin"], m["F"], m["H"], m["concat"])
@@ -82,7 +101,7 @@ CASES = [
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_e%d_fin%d_h%d_f%d_%s_%s" % (
     c[0], c[1], c[2], c[3], c[4], "cat" if c[5] else "mean", c[6]))
-def test_random_vs_oracle(case):
+def test_random_vs_oracle(case, variant):
     n, e, fin, H, F, concat, kind = case
     x, ei, state = random_case(n, e, fin, H, F, concat, seed=n + e + H, kind=kind)
     ref = gat_layer_forward_from_state(state, x, ei, H, concat)
