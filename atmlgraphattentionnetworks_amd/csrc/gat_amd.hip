@@ -56,14 +56,19 @@ int next_pow2(int v) {
 
 // ---------------------------------------------------------------------------
 // Projection: T[:, :HF] = X W^T + b, s_src / s_dst fused in the epilogue.
+// Replaces GAT.py:42-52 (H small Linear GEMMs + 2H attention Linears).
 //
-// One 256-thread workgroup (4 waves) owns BM = 64 node rows and ALL HF output
-// columns (so each head's score dot product stays in the workgroup).  Each
-// wave owns 16 rows x (NT * 16) columns as NT accumulators of
-// v_mfma_f32_16x16x4_f32 (exact fp32, k-ordered fma chain).  X and W tiles
-// are staged through LDS, BK = 32 deep.
+// One 256-thread workgroup (4 waves) owns 64 node rows x ALL NT*16 output
+// columns; each wave owns 16 rows as NT accumulators of
+// v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fma chain).  Per 64-deep
+// K tile the W tile [NT*16 x 64] is staged once in LDS for the 4 waves, and
+// each wave loads its X fragments straight to registers (every X row is read
+// once) — one load round per tile, a single round for Fin <= 64.
+// Epilogue, on the accumulators: + Linear bias, Wh stores, then the two
+// attention dot products per head — xor-shuffles across the head's F lanes
+// when F | 16 or 16 | F (SHFL), else through an LDS copy of the tile.
 // ---------------------------------------------------------------------------
-template <int NT>
+template <int NT, bool SHFL>
 __global__ __launch_bounds__(256) void k_project(
     const float* __restrict__ X, int n, int fin,
     const float* __restrict__ W, const float* __restrict__ bW,
@@ -71,84 +76,148 @@ __global__ __launch_bounds__(256) void k_project(
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ T, int ld, int s_off,
     float* __restrict__ s_dst) {
-    constexpr int BM = 64, BK = 32, BN = NT * 16;
-    constexpr int XS = BK + 2;  // 2-float pad: the 16x16x4 A/B reads are conflict-free
+    constexpr int BK = 64, KS = BK / 4, BN = NT * 16;
+    constexpr int WS = BK + 2;  // 16x16x4 B-fragment reads are conflict-free at this stride
     constexpr int OS = BN + 1;
-    constexpr int MAIN = (BM + BN) * XS;
-    constexpr int EPIL = BM * OS;
-    __shared__ float smem[MAIN > EPIL ? MAIN : EPIL];
-    float* Xs = smem;
-    float* Ws = smem + BM * XS;
+    constexpr int LDS = (BN * WS > 64 * OS) ? BN * WS : 64 * OS;
+    __shared__ float smem[LDS];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int row0 = blockIdx.x * BM;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int row0 = blockIdx.x * 64 + w * 16;
+    const int ar = row0 + cl;
+    const float* xr = X + (size_t)(ar < n ? ar : (n > 0 ? n - 1 : 0)) * fin;
+    const float xs = ar < n ? 1.f : 0.f;
 
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     for (int k0 = 0; k0 < fin; k0 += BK) {
-        for (int idx = tid; idx < BM * BK; idx += 256) {
-            const int rr = idx / BK, kk = idx % BK;
-            const int gr = row0 + rr, gk = k0 + kk;
-            Xs[rr * XS + kk] = (gr < n && gk < fin) ? X[(size_t)gr * fin + gk] : 0.f;
-        }
         for (int idx = tid; idx < BN * BK; idx += 256) {
             const int nn = idx / BK, kk = idx % BK;
             const int gk = k0 + kk;
-            Ws[nn * XS + kk] = (nn < HF && gk < fin) ? W[(size_t)nn * fin + gk] : 0.f;
+            smem[nn * WS + kk] = (nn < HF && gk < fin) ? W[(size_t)nn * fin + gk] : 0.f;
+        }
+        float xa[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int kk = k0 + 4 * s + kq;
+            xa[s] = kk < fin ? xr[kk] * xs : 0.f;
         }
         __syncthreads();
+        const int ksteps = min(KS, (fin - k0 + 3) / 4);
 #pragma unroll
-        for (int ks = 0; ks < BK; ks += 4) {
-            // 16x16x4 f32 operand maps: A[l&15][k=l>>4], B[k=l>>4][l&15]
-            const float a = Xs[(w * 16 + (lane & 15)) * XS + ks + (lane >> 4)];
+        for (int s = 0; s < KS; ++s) {
+            if (s < ksteps) {  // wave-uniform
 #pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const float b = Ws[(t * 16 + (lane & 15)) * XS + ks + (lane >> 4)];
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+                for (int t = 0; t < NT; ++t) {
+                    const float b = smem[(t * 16 + cl) * WS + 4 * s + kq];
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], b, acc[t], 0, 0, 0);
+                }
             }
         }
         __syncthreads();
     }
 
-    // C/D map: col = lane & 15, row = (lane >> 4) * 4 + i
-    float* Os = smem;
+    // accumulator map: column t*16 + cl, rows (lane >> 4) * 4 + i of the wave's 16
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t) {
+        const int cc = t * 16 + cl;
+        const float bb = cc < HF ? bW[cc] : 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            Os[(w * 16 + (lane >> 4) * 4 + i) * OS + t * 16 + (lane & 15)] = acc[t][i];
-    __syncthreads();
-    // + Linear bias b_h (inside Wh, GAT.py:43)
-    for (int idx = tid; idx < BM * HF; idx += 256) {
-        const int rr = idx / HF, cc = idx % HF;
-        Os[rr * OS + cc] += bW[cc];
-    }
-    __syncthreads();
-    for (int idx = tid; idx < BM * s_off; idx += 256) {
-        const int rr = idx / s_off, cc = idx % s_off;
-        const int gr = row0 + rr;
-        if (gr < n) T[(size_t)gr * ld + cc] = cc < HF ? Os[rr * OS + cc] : 0.f;
-    }
-    // attention Linears on the fp32 Wh (GAT.py:44-45): s = Wh_h . a_h + c_h
-    const int sw = ld - s_off;
-    for (int idx = tid; idx < BM * sw; idx += 256) {
-        const int rr = idx / sw, h = idx % sw;
-        const int gr = row0 + rr;
-        if (gr >= n) continue;
-        float s1 = 0.f, s2 = 0.f;
-        if (h < H) {
-            for (int f = 0; f < F; ++f) {
-                const float v = Os[rr * OS + h * F + f];
-                s1 = fmaf(v, a1[h * F + f], s1);
-                s2 = fmaf(v, a2[h * F + f], s2);
-            }
-            s1 += c1[h];
-            s2 += c2[h];
-            s_dst[(size_t)gr * H + h] = s2;
+        for (int i = 0; i < 4; ++i) {
+            const float v = acc[t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
+            acc[t][i] = v;
+            const int rr = row0 + (lane >> 4) * 4 + i;
+            if (rr < n && cc < s_off) T[(size_t)rr * ld + cc] = v;
         }
-        T[(size_t)gr * ld + s_off + h] = s1;
+    }
+
+    if constexpr (SHFL) {
+        if (F <= 16) {  // head = F consecutive lanes of one tile: reduce tile by tile
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int cc = t * 16 + cl;
+                const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
+                float p1[4], p2[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    p1[i] = acc[t][i] * w1;
+                    p2[i] = acc[t][i] * w2;
+                }
+                for (int off = 1; off < F; off <<= 1)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        p1[i] += __shfl_xor(p1[i], off);
+                        p2[i] += __shfl_xor(p2[i], off);
+                    }
+                const int h = cc / F;
+                if ((cl & (F - 1)) == 0 && h < H) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int rr = row0 + (lane >> 4) * 4 + i;
+                        if (rr >= n) continue;
+                        T[(size_t)rr * ld + s_off + h] = p1[i] + c1[h];
+                        s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
+                    }
+                }
+            }
+        } else {  // 16 | F: head h spans tiles [h*F/16, (h+1)*F/16)
+            const int tph = F / 16;
+            float p1[4] = {0.f, 0.f, 0.f, 0.f}, p2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int cc = t * 16 + cl;
+                const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    p1[i] += acc[t][i] * w1;
+                    p2[i] += acc[t][i] * w2;
+                }
+                if ((t + 1) % tph == 0) {  // last tile of head h
+                    const int h = t / tph;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        for (int off = 1; off < 16; off <<= 1) {
+                            p1[i] += __shfl_xor(p1[i], off);
+                            p2[i] += __shfl_xor(p2[i], off);
+                        }
+                    if (cl == 0 && h < H) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int rr = row0 + (lane >> 4) * 4 + i;
+                            if (rr >= n) continue;
+                            T[(size_t)rr * ld + s_off + h] = p1[i] + c1[h];
+                            s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) p1[i] = p2[i] = 0.f;
+                }
+            }
+        }
+    } else {
+        // any F: the wave's 16 x BN tile through LDS, one (row, head) per lane-iteration
+        float* Os = smem + w * 16 * OS;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Os[((lane >> 4) * 4 + i) * OS + t * 16 + cl] = acc[t][i];
+        __syncthreads();
+        for (int idx = lane; idx < 16 * H; idx += kWave) {
+            const int rl = idx / H, h = idx % H;
+            const int rr = row0 + rl;
+            if (rr >= n) continue;
+            float v1 = 0.f, v2 = 0.f;
+            for (int f = 0; f < F; ++f) {
+                const float v = Os[rl * OS + h * F + f];
+                v1 = fmaf(v, a1[h * F + f], v1);
+                v2 = fmaf(v, a2[h * F + f], v2);
+            }
+            T[(size_t)rr * ld + s_off + h] = v1 + c1[h];
+            s_dst[(size_t)rr * H + h] = v2 + c2[h];
+        }
     }
 }
 
@@ -300,145 +369,6 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 }
 
 // ---------------------------------------------------------------------------
-// Projection, register-direct variant (F divides 16 or F % 16 == 0).
-//
-// Each wave owns 16 node rows x all NT*16 columns.  MFMA A/B fragments are
-// loaded straight from global memory (W is a few KB and stays in L1/L2; each
-// X row is read once), so the kernel has no LDS and no barriers.  The
-// epilogue works on the accumulators in place: bias add, Wh stores, and the
-// two attention dot products reduced across the F lanes of each head with
-// xor-shuffles (F | 16) or across whole tiles then 16 lanes (F % 16 == 0).
-// ---------------------------------------------------------------------------
-template <int NT>
-__global__ __launch_bounds__(256) void k_project_reg(
-    const float* __restrict__ X, int n, int fin,
-    const float* __restrict__ W, const float* __restrict__ bW,
-    const float* __restrict__ a1, const float* __restrict__ c1,
-    const float* __restrict__ a2, const float* __restrict__ c2,
-    int H, int F, int HF, float* __restrict__ T, int ld, int s_off,
-    float* __restrict__ s_dst) {
-    constexpr int KU = 4;  // k-steps (of 4) per unrolled block
-    const int lane = threadIdx.x & 63;
-    const int row0 = (blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6)) * 16;
-    if (row0 >= n) return;
-    const int cl = lane & 15, kq = lane >> 4;
-    const int ar = row0 + cl;
-    const float* xr = X + (size_t)(ar < n ? ar : n - 1) * fin;
-    const float xs = ar < n ? 1.f : 0.f;
-    const float* wr[NT];
-    float ws[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int cc = t * 16 + cl;
-        wr[t] = W + (size_t)(cc < HF ? cc : 0) * fin;
-        ws[t] = cc < HF ? 1.f : 0.f;
-    }
-    f32x4 acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    int k = 0;
-    for (; k + 4 * KU <= fin; k += 4 * KU) {
-        float a[KU], b[KU][NT];
-#pragma unroll
-        for (int u = 0; u < KU; ++u) {
-            a[u] = xr[k + 4 * u + kq] * xs;
-#pragma unroll
-            for (int t = 0; t < NT; ++t) b[u][t] = wr[t][k + 4 * u + kq] * ws[t];
-        }
-#pragma unroll
-        for (int u = 0; u < KU; ++u)
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u][t], acc[t], 0, 0, 0);
-    }
-    for (; k < fin; k += 4) {
-        const int kk = k + kq;
-        const bool ok = kk < fin;
-        const float a = ok ? xr[kk] * xs : 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const float b = ok ? wr[t][kk] * ws[t] : 0.f;
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
-        }
-    }
-
-    // accumulator map: column t*16 + cl, rows (lane >> 4) * 4 + i
-    float s1[NT][4], s2[NT][4];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int cc = t * 16 + cl;
-        const bool cv = cc < HF;
-        const float bb = cv ? bW[cc] : 0.f;
-        const float w1 = cv ? a1[cc] : 0.f, w2 = cv ? a2[cc] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float v = acc[t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
-            acc[t][i] = v;
-            s1[t][i] = v * w1;
-            s2[t][i] = v * w2;
-            const int rr = row0 + (lane >> 4) * 4 + i;
-            if (rr < n && cc < s_off) T[(size_t)rr * ld + cc] = v;
-        }
-    }
-    if (F <= 16) {
-        // head = F consecutive lanes of one tile
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                for (int off = 1; off < F; off <<= 1) {
-                    s1[t][i] += __shfl_xor(s1[t][i], off);
-                    s2[t][i] += __shfl_xor(s2[t][i], off);
-                }
-        if ((cl & (F - 1)) == 0) {
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const int h = (t * 16 + cl) / F;
-                if (h >= H) continue;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int rr = row0 + (lane >> 4) * 4 + i;
-                    if (rr >= n) continue;
-                    T[(size_t)rr * ld + s_off + h] = s1[t][i] + c1[h];
-                    s_dst[(size_t)rr * H + h] = s2[t][i] + c2[h];
-                }
-            }
-        }
-    } else {
-        // F % 16 == 0: head h spans tiles [h*F/16, (h+1)*F/16)
-        const int tph = F / 16;
-        for (int h = 0; h < H; ++h) {
-            float p1[4] = {0.f, 0.f, 0.f, 0.f}, p2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                if (t / tph != h) continue;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    p1[i] += s1[t][i];
-                    p2[i] += s2[t][i];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                for (int off = 1; off < 16; off <<= 1) {
-                    p1[i] += __shfl_xor(p1[i], off);
-                    p2[i] += __shfl_xor(p2[i], off);
-                }
-            if (cl == 0) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int rr = row0 + (lane >> 4) * 4 + i;
-                    if (rr >= n) continue;
-                    T[(size_t)rr * ld + s_off + h] = p1[i] + c1[h];
-                    s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
-                }
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Edge kernel, lane-group variant (F % 4 == 0): G = next_pow2(HF/4) lanes per
 // target row, 64/G rows per wave, one row per group.
 //
@@ -450,8 +380,8 @@ __global__ __launch_bounds__(256) void k_project_reg(
 // rescale per chunk.  Head mean (concat=False, F/4 a power of two) is an
 // xor-butterfly over the group.
 // ---------------------------------------------------------------------------
-template <int G, int U>
-__global__ __launch_bounds__(256) void k_edge_grp(
+template <int G, int U, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_edge_grp(
     const int* __restrict__ rowptr, const int* __restrict__ col, int row_begin, int row_end,
     const float* __restrict__ T, int ld, int s_off, const float* __restrict__ s_dst,
     int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
@@ -647,16 +577,18 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
     const int nt = (hf + 15) / 16;
-    const bool reg_ok = (f <= 16 && 16 % f == 0) || (f % 16 == 0);
-    const bool use_reg = reg_ok && kernel_choice("GAT_PROJ_KERNEL", "reg", "generic");
+    const bool shfl = ((f <= 16 && 16 % f == 0) || (f % 16 == 0)) &&
+                      kernel_choice("GAT_PROJ_KERNEL", "shfl", "lds");
 #define GAT_PROJ_CASE(NT)                                                                   \
     case NT:                                                                                \
-        if (use_reg)                                                                        \
-            hipLaunchKernelGGL(k_project_reg<NT>, grid, block, 0, st, x, n, fin, w, b, a_src, \
-                               c_src, a_dst, c_dst, heads, f, hf, table, ld, s_off, s_dst);  \
+        if (shfl)                                                                           \
+            hipLaunchKernelGGL((k_project<NT, true>), grid, block, 0, st, x, n, fin, w, b,   \
+                               a_src, c_src, a_dst, c_dst, heads, f, hf, table, ld, s_off,  \
+                               s_dst);                                                      \
         else                                                                                \
-            hipLaunchKernelGGL(k_project<NT>, grid, block, 0, st, x, n, fin, w, b, a_src,   \
-                               c_src, a_dst, c_dst, heads, f, hf, table, ld, s_off, s_dst);  \
+            hipLaunchKernelGGL((k_project<NT, false>), grid, block, 0, st, x, n, fin, w, b,  \
+                               a_src, c_src, a_dst, c_dst, heads, f, hf, table, ld, s_off,  \
+                               s_dst);                                                      \
         break;
     switch (nt) {
         GAT_PROJ_CASE(1) GAT_PROJ_CASE(2) GAT_PROJ_CASE(3) GAT_PROJ_CASE(4)
@@ -686,16 +618,22 @@ int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row
     const bool grp_ok = (f % 4 == 0) && (concat || pow2_f4);
     if (grp_ok && kernel_choice("GAT_EDGE_KERNEL", "group", "generic")) {
         const int u = edge_unroll();
+        const bool occ8 = std::getenv("GAT_EDGE_OCC8") != nullptr;
         const long long threads = (long long)rows * g;
         const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
 #define GAT_GRP_LAUNCH(G, UU)                                                                  \
-    hipLaunchKernelGGL((k_edge_grp<G, UU>), grid, block, 0, st, rowptr, col, row_begin,        \
-                       row_end, table, ld, s_off, s_dst, heads, f, hf, concat, negative_slope, \
-                       bias, out, ld_out, lse)
-#define GAT_GRP_U(G)                          \
-    if (u == 4) GAT_GRP_LAUNCH(G, 4);         \
-    else if (u == 16) GAT_GRP_LAUNCH(G, 16);  \
-    else GAT_GRP_LAUNCH(G, 8);
+    if (occ8)                                                                                  \
+        hipLaunchKernelGGL((k_edge_grp<G, UU, 8>), grid, block, 0, st, rowptr, col, row_begin, \
+                           row_end, table, ld, s_off, s_dst, heads, f, hf, concat,             \
+                           negative_slope, bias, out, ld_out, lse);                            \
+    else                                                                                       \
+        hipLaunchKernelGGL((k_edge_grp<G, UU, 1>), grid, block, 0, st, rowptr, col, row_begin, \
+                           row_end, table, ld, s_off, s_dst, heads, f, hf, concat,             \
+                           negative_slope, bias, out, ld_out, lse)
+#define GAT_GRP_U(G)                            \
+    if (u == 4) { GAT_GRP_LAUNCH(G, 4); }       \
+    else if (u == 16) { GAT_GRP_LAUNCH(G, 16); } \
+    else { GAT_GRP_LAUNCH(G, 8); }
         switch (g) {
             case 1: GAT_GRP_U(1) break;
             case 2: GAT_GRP_U(2) break;

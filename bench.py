@@ -168,10 +168,14 @@ def main():
         ev1.record(stream)
         ev1.synchronize()
         edge_ms = ev0.elapsed_time(ev1) / args.edge_iters
-        # projection alone
+        # projection alone: short kernel, so time launches captured in a graph
+        gp = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gp):
+            for _ in range(args.edge_iters):
+                project(x, pp, w.heads, w.out_channels, table=table, s_dst=s_dst)
+        gp.replay()
         ev0.record(stream)
-        for _ in range(args.edge_iters):
-            project(x, pp, w.heads, w.out_channels, table=table, s_dst=s_dst)
+        gp.replay()
         ev1.record(stream)
         ev1.synchronize()
         proj_ms = ev0.elapsed_time(ev1) / args.edge_iters

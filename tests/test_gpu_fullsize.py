@@ -1,0 +1,56 @@
+"""Parity at BASELINE.json's full sizes.
+
+PPI-shape is checked in full in test_gpu_parity.py.  Here: arxiv-scale and the
+CIFAR10 superpixel batch in full against the oracle, and Reddit-scale
+(N=232,965, E=114,615,892, Fin=602) by sampled rows: the oracle evaluates the
+complete in-edge set of 64 random targets (plus every node's self-loop), which
+gives those rows' exact reference outputs without materialising the 29 GB
+[E', H, F] message tensor on the host.
+"""
+import pytest
+import torch
+
+from oracle import gat_layer_forward_from_state, init_reference_params
+
+pytestmark = pytest.mark.gpu
+
+ATOL = RTOL = 1e-5
+
+
+def _layer(w, dev, state):
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads, concat=w.concat)
+    layer.load_state_dict(state)
+    return layer.to(dev).eval()
+
+
+@pytest.mark.parametrize("name", ["arxiv", "cifar", "cifar_h8", "ppi_h4"])
+def test_full_workload_vs_oracle(name):
+    from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
+    dev = torch.device("cuda", 0)
+    w = WORKLOADS[name]
+    x, ei = make_inputs(w, dev)
+    state = init_reference_params(w.in_channels, w.out_channels, w.heads, w.concat, seed=0)
+    with torch.no_grad():
+        out = _layer(w, dev, state)(x, ei).cpu()
+    ref = gat_layer_forward_from_state(state, x.cpu(), ei.cpu(), w.heads, w.concat)
+    torch.testing.assert_close(out, ref, atol=ATOL, rtol=RTOL)
+
+
+def test_reddit_scale_sampled_rows():
+    from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
+    dev = torch.device("cuda", 0)
+    w = WORKLOADS["reddit"]
+    x, ei = make_inputs(w, dev)
+    state = init_reference_params(w.in_channels, w.out_channels, w.heads, w.concat, seed=0)
+    with torch.no_grad():
+        out = _layer(w, dev, state)(x, ei)
+    g = torch.Generator(device="cpu")
+    g.manual_seed(123)
+    rows = torch.randperm(x.size(0), generator=g)[:64].to(dev)
+    keep = torch.isin(ei[1], rows)
+    sub = ei[:, keep].cpu()
+    assert sub.size(1) > 64 * 300  # ~493 in-edges per row at this shape
+    ref = gat_layer_forward_from_state(state, x.cpu(), sub, w.heads, w.concat)
+    rc = rows.cpu()
+    torch.testing.assert_close(out[rows].cpu(), ref[rc], atol=ATOL, rtol=RTOL)

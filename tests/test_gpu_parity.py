@@ -26,7 +26,7 @@ def dev():
 # shape allows) AND on the generic kernels, selected by the library's env knobs.
 VARIANTS = {
     "fast": {},
-    "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "generic"},
+    "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds"},
     "fast_u4": {"GAT_EDGE_U": "4"},
     "fast_u16": {"GAT_EDGE_U": "16"},
 }

@@ -20,26 +20,36 @@ EDGE_VARIANTS = {
     "grp_u4": {"GAT_EDGE_U": "4"},
     "grp_u8": {"GAT_EDGE_U": "8"},
     "grp_u16": {"GAT_EDGE_U": "16"},
+    "grp_u8_occ8": {"GAT_EDGE_U": "8", "GAT_EDGE_OCC8": "1"},
+    "grp_u4_occ8": {"GAT_EDGE_U": "4", "GAT_EDGE_OCC8": "1"},
 }
-PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "generic"}, "reg": {}}
+PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "shfl": {}}
 
 
 def set_env(d):
-    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U"):
+    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_OCC8"):
         os.environ.pop(k, None)
     os.environ.update(d)
 
 
-def time_fn(fn, iters):
+def time_fn(fn, iters, reps=3):
+    """Average GPU time per call: `iters` calls captured in one HIP graph and
+    replayed, so host launch overhead does not leak into short kernels."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn()
     e0.record(s)
-    for _ in range(iters):
-        fn()
+    for _ in range(reps):
+        g.replay()
     e1.record(s)
     e1.synchronize()
-    return e0.elapsed_time(e1) / iters
+    return e0.elapsed_time(e1) / (iters * reps)
 
 
 def main():
