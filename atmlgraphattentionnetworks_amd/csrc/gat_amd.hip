@@ -11,11 +11,14 @@
 //                          (GAT.py:53-67, PyG utils.softmax, aggr='add')
 //
 // Data layout in HBM (see DESIGN.md "Data layout"):
-//   node table T[n_nodes][ld] fp32, one row per SOURCE node:
-//       [0, HF)        Wh = x W^T + b   (head-major: column h*F+f)
-//       [HF, s_off)    zero pad, s_off = round_up(HF, 4)
-//       [s_off, +H)    s_src[h] = Wh_h . a1_h + c1_h
-//       [s_off+H, ld)  zero pad, ld = s_off + round_up(H, 4)
+//   Wh[n_nodes][ld_wh] fp32, one row per SOURCE node, Wh = x W^T + b,
+//       head-major (column h*F+f), zero-padded to round_up(HF, 4) columns;
+//       ld_wh % 4 == 0 so every row is 16-B aligned (HF = 64: one 256-B row =
+//       exactly two 128-B lines per gathered edge).
+//   s_src[n_nodes] at stride ld_s (>= H): Wh_h . a1_h + c1_h (source term).
+//       Default layout: its own compact [N][H] array (PPI: 1.4 MB, L2-resident).
+//       Packed layout (one all-gather for multi-GPU): s_src = Wh + s_off with
+//       ld_s = ld_wh (gat_table_layout).
 //   s_dst[n_nodes][H] fp32 (target term, read once per row)
 //   CSR by target: rowptr int32 [n+1], col int32 [E+n]; within a row the
 //   input edge order is kept (stable sort) and the self-loop is last,
@@ -55,7 +58,7 @@ int next_pow2(int v) {
 }
 
 // ---------------------------------------------------------------------------
-// Projection: T[:, :HF] = X W^T + b, s_src / s_dst fused in the epilogue.
+// Projection: Wh = X W^T + b, s_src / s_dst fused in the epilogue.
 // Replaces GAT.py:42-52 (H small Linear GEMMs + 2H attention Linears).
 //
 // One 256-thread workgroup (4 waves) owns 64 node rows x ALL NT*16 output
@@ -74,9 +77,11 @@ __global__ __launch_bounds__(256) void k_project(
     const float* __restrict__ W, const float* __restrict__ bW,
     const float* __restrict__ a1, const float* __restrict__ c1,
     const float* __restrict__ a2, const float* __restrict__ c2,
-    int H, int F, int HF, float* __restrict__ T, int ld, int s_off,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
     float* __restrict__ s_dst) {
     constexpr int BK = 64, KS = BK / 4, BN = NT * 16;
+    constexpr int WL = BN * BK / 256;      // W-tile elements per thread
+    constexpr int WB = WL < 16 ? WL : 16;  // loads kept in flight per batch
     constexpr int WS = BK + 2;  // 16x16x4 B-fragment reads are conflict-free at this stride
     constexpr int OS = BN + 1;
     constexpr int LDS = (BN * WS > 64 * OS) ? BN * WS : 64 * OS;
@@ -93,11 +98,24 @@ __global__ __launch_bounds__(256) void k_project(
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    const int hfp = round_up4(HF);
     for (int k0 = 0; k0 < fin; k0 += BK) {
-        for (int idx = tid; idx < BN * BK; idx += 256) {
-            const int nn = idx / BK, kk = idx % BK;
-            const int gk = k0 + kk;
-            smem[nn * WS + kk] = (nn < HF && gk < fin) ? W[(size_t)nn * fin + gk] : 0.f;
+        // W tile -> LDS: batches of WB independent loads, then their stores
+        // (a plain idx loop would wait on every load before its ds_write)
+#pragma unroll
+        for (int b0 = 0; b0 < WL; b0 += WB) {
+            float wv[WB];
+#pragma unroll
+            for (int q = 0; q < WB; ++q) {
+                const int idx = tid + (b0 + q) * 256;
+                const int nn = idx / BK, gk = k0 + idx % BK;
+                wv[q] = (nn < HF && gk < fin) ? W[(size_t)nn * fin + gk] : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < WB; ++q) {
+                const int idx = tid + (b0 + q) * 256;
+                smem[(idx / BK) * WS + idx % BK] = wv[q];
+            }
         }
         float xa[KS];
 #pragma unroll
@@ -130,7 +148,7 @@ __global__ __launch_bounds__(256) void k_project(
             const float v = acc[t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
             acc[t][i] = v;
             const int rr = row0 + (lane >> 4) * 4 + i;
-            if (rr < n && cc < s_off) T[(size_t)rr * ld + cc] = v;
+            if (rr < n && cc < hfp) Wh[(size_t)rr * ld_wh + cc] = v;
         }
     }
 
@@ -158,7 +176,7 @@ __global__ __launch_bounds__(256) void k_project(
                     for (int i = 0; i < 4; ++i) {
                         const int rr = row0 + (lane >> 4) * 4 + i;
                         if (rr >= n) continue;
-                        T[(size_t)rr * ld + s_off + h] = p1[i] + c1[h];
+                        Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
                         s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
                     }
                 }
@@ -188,7 +206,7 @@ __global__ __launch_bounds__(256) void k_project(
                         for (int i = 0; i < 4; ++i) {
                             const int rr = row0 + (lane >> 4) * 4 + i;
                             if (rr >= n) continue;
-                            T[(size_t)rr * ld + s_off + h] = p1[i] + c1[h];
+                            Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
                             s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
                         }
                     }
@@ -215,7 +233,7 @@ __global__ __launch_bounds__(256) void k_project(
                 v1 = fmaf(v, a1[h * F + f], v1);
                 v2 = fmaf(v, a2[h * F + f], v2);
             }
-            T[(size_t)rr * ld + s_off + h] = v1 + c1[h];
+            Ss[(size_t)rr * ld_s + h] = v1 + c1[h];
             s_dst[(size_t)rr * H + h] = v2 + c2[h];
         }
     }
@@ -238,7 +256,8 @@ __global__ __launch_bounds__(256) void k_project(
 template <int LPE, int HP>
 __global__ __launch_bounds__(64) void k_edge_fwd(
     const int* __restrict__ rowptr, const int* __restrict__ col, int row_begin, int row_end,
-    const float* __restrict__ T, int ld, int s_off, const float* __restrict__ s_dst,
+    const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
+    const float* __restrict__ s_dst,
     int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
     float* __restrict__ out, int ld_out, float* __restrict__ lse) {
     constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;  // edges per chunk
@@ -287,7 +306,7 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
             float e = -INFINITY;
             if (k < nk && hs_ok) {
                 const int j = col_s[k];
-                e = leaky(sd + T[(size_t)j * ld + s_off + hs], slope);
+                e = leaky(sd + Ss[(size_t)j * ld_s + hs], slope);
             }
             ev[q] = e;
             mloc = fmaxf(mloc, e);
@@ -321,7 +340,7 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
                 const bool ok = k < nk;
                 const int kk = ok ? k : nk - 1;
                 const int j = col_s[kk];
-                v[u] = *reinterpret_cast<const f32x4*>(T + (size_t)j * ld + coff);
+                v[u] = *reinterpret_cast<const f32x4*>(Wh + (size_t)j * ld_wh + coff);
                 const float* pr = p_s + kk * HP;
                 const float g = ok ? 1.f : 0.f;
                 pv[u] = f32x4{pr[hq[0]] * g, pr[hq[1]] * g, pr[hq[2]] * g, pr[hq[3]] * g};
@@ -383,7 +402,8 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 template <int G, int U, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_edge_grp(
     const int* __restrict__ rowptr, const int* __restrict__ col, int row_begin, int row_end,
-    const float* __restrict__ T, int ld, int s_off, const float* __restrict__ s_dst,
+    const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
+    const float* __restrict__ s_dst,
     int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
     float* __restrict__ out, int ld_out, float* __restrict__ lse) {
     constexpr int CL = (U + G - 1) / G;  // col values held per lane per chunk
@@ -415,9 +435,9 @@ __global__ __launch_bounds__(256, MINW) void k_edge_grp(
         f32x4 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const size_t row = (size_t)(j[u] >= 0 ? j[u] : j[0]) * ld;
-            s[u] = T[row + s_off + h];
-            v[u] = *reinterpret_cast<const f32x4*>(T + row + coff);
+            const size_t jj = (size_t)(j[u] >= 0 ? j[u] : j[0]);
+            s[u] = Ss[jj * ld_s + h];
+            v[u] = *reinterpret_cast<const f32x4*>(Wh + jj * ld_wh + coff);
         }
         float emax = -INFINITY;
 #pragma unroll
@@ -568,11 +588,12 @@ int gat_table_layout(int heads, int f, int* ld, int* s_off) {
 
 int gat_project(const float* x, int n, int fin, const float* w, const float* b,
                 const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,
-                int heads, int f, float* table, int ld, int s_off, float* s_dst, void* stream) {
+                int heads, int f, float* wh, int ld_wh, float* s_src, int ld_s, float* s_dst,
+                void* stream) {
     if (n < 0 || fin < 0 || heads <= 0 || f <= 0) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
-    if (s_off < hf || (s_off & 3) || ld < s_off + heads || (ld & 3)) return GAT_EINVAL;
+    if (ld_wh < round_up4(hf) || (ld_wh & 3) || ld_s < heads) return GAT_EINVAL;
     if (n == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
@@ -583,12 +604,12 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     case NT:                                                                                \
         if (shfl)                                                                           \
             hipLaunchKernelGGL((k_project<NT, true>), grid, block, 0, st, x, n, fin, w, b,   \
-                               a_src, c_src, a_dst, c_dst, heads, f, hf, table, ld, s_off,  \
-                               s_dst);                                                      \
+                               a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src,  \
+                               ld_s, s_dst);                                                \
         else                                                                                \
             hipLaunchKernelGGL((k_project<NT, false>), grid, block, 0, st, x, n, fin, w, b,  \
-                               a_src, c_src, a_dst, c_dst, heads, f, hf, table, ld, s_off,  \
-                               s_dst);                                                      \
+                               a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src,  \
+                               ld_s, s_dst);                                                \
         break;
     switch (nt) {
         GAT_PROJ_CASE(1) GAT_PROJ_CASE(2) GAT_PROJ_CASE(3) GAT_PROJ_CASE(4)
@@ -602,13 +623,13 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
 }
 
 int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row_end,
-                       const float* table, int ld, int s_off, const float* s_dst, int heads,
-                       int f, int concat, float negative_slope, const float* bias, float* out,
-                       float* lse, void* stream) {
+                       const float* wh, int ld_wh, const float* s_src, int ld_s,
+                       const float* s_dst, int heads, int f, int concat, float negative_slope,
+                       const float* bias, float* out, float* lse, void* stream) {
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
-    if (s_off < hf || (s_off & 3) || ld < s_off + heads || (ld & 3)) return GAT_EINVAL;
+    if (ld_wh < round_up4(hf) || (ld_wh & 3) || ld_s < heads) return GAT_EINVAL;
     const int rows = row_end - row_begin;
     if (rows == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
@@ -624,11 +645,11 @@ int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row
 #define GAT_GRP_LAUNCH(G, UU)                                                                  \
     if (occ8)                                                                                  \
         hipLaunchKernelGGL((k_edge_grp<G, UU, 8>), grid, block, 0, st, rowptr, col, row_begin, \
-                           row_end, table, ld, s_off, s_dst, heads, f, hf, concat,             \
+                           row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,             \
                            negative_slope, bias, out, ld_out, lse);                            \
     else                                                                                       \
         hipLaunchKernelGGL((k_edge_grp<G, UU, 1>), grid, block, 0, st, rowptr, col, row_begin, \
-                           row_end, table, ld, s_off, s_dst, heads, f, hf, concat,             \
+                           row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,             \
                            negative_slope, bias, out, ld_out, lse)
 #define GAT_GRP_U(G)                            \
     if (u == 4) { GAT_GRP_LAUNCH(G, 4); }       \
@@ -653,7 +674,7 @@ int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row
     const dim3 grid(rows), block(kWave);
 #define GAT_EDGE_LAUNCH(L, P)                                                                \
     hipLaunchKernelGGL((k_edge_fwd<L, P>), grid, block, 0, st, rowptr, col, row_begin,       \
-                       row_end, table, ld, s_off, s_dst, heads, f, hf, concat,              \
+                       row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,              \
                        negative_slope, bias, out, ld_out, lse)
 #define GAT_EDGE_HP(L)                                                                       \
     switch (hp) {                                                                            \

@@ -32,7 +32,6 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
-from . import _lib
 
 
 def partition_rows(rowptr: torch.Tensor, parts: int) -> List[int]:
@@ -67,6 +66,11 @@ def remap_to_table(col: torch.Tensor, bounds: List[int], rows_per_part: int) -> 
 
 class HipOps:
     """The HIP kernels (default)."""
+
+    @staticmethod
+    def alloc_table(n, heads, f, device, packed=True):
+        from .layer import alloc_table
+        return alloc_table(n, heads, f, device, packed=packed)
 
     @staticmethod
     def project(x, pp, heads, f, table, s_dst):
@@ -109,11 +113,11 @@ class ShardedGAT:
             n_table = csr.num_nodes
         self.local = LocalCSR((rp[self.r0:self.r1 + 1] - e0).to(torch.int32).contiguous(),
                               col.contiguous(), self.n_local, e1 - e0)
-        ld, _ = _lib.table_layout(self.heads, self.f) if isinstance(self.ops, type) and \
-            self.ops is HipOps else self.ops.table_layout(self.heads, self.f)
-        self.ld = ld
-        # zero-filled so padding rows of a slot are defined (never referenced)
-        self.table = torch.zeros(n_table, ld, dtype=torch.float32, device=dev)
+        # allgather: one packed buffer [Wh | s_src] per node row, so a single
+        # collective moves both (zero-filled: padding rows are defined);
+        # replicate: the default separate layout (no collective to feed)
+        self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev,
+                                          packed=(exchange == "allgather"))
         self.s_dst_full = torch.empty(csr.num_nodes if exchange == "replicate" else self.n_local,
                                       self.heads, dtype=torch.float32, device=dev)
         width = self.heads * self.f if self.concat else self.f
@@ -122,8 +126,8 @@ class ShardedGAT:
     # -- the three phases of a step (split so compute can be graph-captured) --
     def phase_project(self, x):
         if self.exchange == "allgather":
-            slot = self.table[self.rank * self.rows_per_part:
-                              self.rank * self.rows_per_part + self.n_local]
+            m = self.rows_per_part
+            slot = self.table.rows(self.rank * m, self.rank * m + self.n_local)
             self.ops.project(x, self.pp, self.heads, self.f, slot, self.s_dst_full)
         else:
             self.ops.project(x, self.pp, self.heads, self.f, self.table, self.s_dst_full)
@@ -131,7 +135,8 @@ class ShardedGAT:
     def phase_exchange(self):
         if self.exchange == "allgather" and self.world > 1:
             m = self.rows_per_part
-            dist.all_gather_into_tensor(self.table, self.table[self.rank * m:(self.rank + 1) * m],
+            buf = self.table.buf
+            dist.all_gather_into_tensor(buf, buf[self.rank * m:(self.rank + 1) * m],
                                         group=self.group)
 
     def phase_edges(self):

@@ -16,14 +16,15 @@ No PyG import, no CPU path: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import NamedTuple, Optional, Tuple
 
 import torch
 
 from . import _lib
 from .graph import CSRGraph, get_csr
 
-__all__ = ["GraphAttentionLayer", "PackedParams", "pack_params", "gat_forward"]
+__all__ = ["GraphAttentionLayer", "PackedParams", "pack_params", "gat_forward", "NodeTable",
+           "alloc_table", "project", "edge_aggregate"]
 
 
 class PackedParams:
@@ -63,39 +64,68 @@ def _stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+class NodeTable(NamedTuple):
+    """Per-source-node outputs of the projection, as the edge kernel reads
+    them: Wh rows (stride ld_wh floats) and s_src (stride ld_s floats).
+
+    Default layout: Wh [N, round_up(H*F, 4)] and a compact s_src [N, H].
+    Packed layout (``packed=True``): one buffer [N, ld] holding both (one
+    collective moves both; see distributed.py), ``buf`` is that buffer."""
+    wh: torch.Tensor
+    ld_wh: int
+    s_src: torch.Tensor
+    ld_s: int
+    buf: Optional[torch.Tensor] = None
+
+    def rows(self, start: int, stop: int) -> "NodeTable":
+        """The table restricted to rows [start, stop) (views, same strides)."""
+        return NodeTable(self.wh[start:stop], self.ld_wh, self.s_src[start:stop], self.ld_s,
+                         None if self.buf is None else self.buf[start:stop])
+
+
+def alloc_table(n: int, heads: int, f: int, device, packed: bool = False) -> NodeTable:
+    if packed:
+        ld, s_off = _lib.table_layout(heads, f)
+        buf = torch.zeros(n, ld, dtype=torch.float32, device=device)
+        return NodeTable(buf, ld, buf[:, s_off:], ld, buf)
+    hfp = (heads * f + 3) // 4 * 4
+    wh = torch.empty(n, hfp, dtype=torch.float32, device=device)
+    s_src = torch.empty(n, heads, dtype=torch.float32, device=device)
+    return NodeTable(wh, hfp, s_src, heads)
+
+
 def project(x: torch.Tensor, pp: PackedParams, heads: int, f: int,
-            table: Optional[torch.Tensor] = None, s_dst: Optional[torch.Tensor] = None):
-    """``gat_project``: node table [N, ld] (Wh | s_src) and s_dst [N, H]."""
+            table: Optional[NodeTable] = None, s_dst: Optional[torch.Tensor] = None):
+    """``gat_project``: node table (Wh, s_src) and s_dst [N, H]."""
     lib = _lib.load()
     n, fin = x.shape
-    ld, s_off = _lib.table_layout(heads, f)
     if table is None:
-        table = torch.empty(n, ld, dtype=torch.float32, device=x.device)
+        table = alloc_table(n, heads, f, x.device)
     if s_dst is None:
         s_dst = torch.empty(n, heads, dtype=torch.float32, device=x.device)
     _lib.check(lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                               pp.c_dst.data_ptr(), heads, f, table.data_ptr(), ld, s_off,
-                               s_dst.data_ptr(), _stream(x.device)), "gat_project")
+                               pp.c_dst.data_ptr(), heads, f, table.wh.data_ptr(), table.ld_wh,
+                               table.s_src.data_ptr(), table.ld_s, s_dst.data_ptr(),
+                               _stream(x.device)), "gat_project")
     return table, s_dst
 
 
-def edge_aggregate(csr: CSRGraph, table: torch.Tensor, s_dst: torch.Tensor, heads: int, f: int,
+def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: int,
                    concat: bool, bias: torch.Tensor, negative_slope: float = 0.2,
                    row_begin: int = 0, row_end: Optional[int] = None,
                    out: Optional[torch.Tensor] = None, lse: Optional[torch.Tensor] = None):
     """``gat_edge_aggregate`` over target rows [row_begin, row_end)."""
     lib = _lib.load()
     rows = csr.num_nodes if row_end is None else row_end
-    ld, s_off = _lib.table_layout(heads, f)
     width = heads * f if concat else f
     if out is None:
-        out = torch.empty(rows, width, dtype=torch.float32, device=table.device)
+        out = torch.empty(rows, width, dtype=torch.float32, device=table.wh.device)
     _lib.check(lib.gat_edge_aggregate(
-        csr.rowptr.data_ptr(), csr.col.data_ptr(), row_begin, rows, table.data_ptr(), ld, s_off,
-        s_dst.data_ptr(), heads, f, int(concat), float(negative_slope), bias.data_ptr(),
-        out.data_ptr(), 0 if lse is None else lse.data_ptr(), _stream(table.device)),
-        "gat_edge_aggregate")
+        csr.rowptr.data_ptr(), csr.col.data_ptr(), row_begin, rows, table.wh.data_ptr(),
+        table.ld_wh, table.s_src.data_ptr(), table.ld_s, s_dst.data_ptr(), heads, f,
+        int(concat), float(negative_slope), bias.data_ptr(), out.data_ptr(),
+        0 if lse is None else lse.data_ptr(), _stream(table.wh.device)), "gat_edge_aggregate")
     return out
 
 

@@ -102,7 +102,7 @@ def main():
         return bench_distributed(args, METRIC)
 
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
-    from atmlgraphattentionnetworks_amd.layer import edge_aggregate, project
+    from atmlgraphattentionnetworks_amd.layer import alloc_table, edge_aggregate, project
     from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
 
     dev = torch.device("cuda", 0)

@@ -45,10 +45,11 @@ extern "C" {
 int gat_abi_version(void);
 
 /*
- * Node-table layout for (heads, f): row stride `ld` floats and the column
- * `s_off` where s_src starts.  Row n = [Wh[n] (heads*f) | 0-pad | s_src[n] (heads) | 0-pad],
- * both parts 16-byte aligned.  Wh is head-major (column h*f + k), i.e. the
- * reference's stack/transpose [N,H,F] view (GAT.py:49-50) made contiguous.
+ * Packed node-table layout for (heads, f): row stride `ld` floats and column
+ * `s_off` where s_src starts, for callers that keep Wh and s_src in ONE buffer
+ * (e.g. to all-gather both with a single collective): pass wh = table,
+ * ld_wh = ld, s_src = table + s_off, ld_s = ld.  Row n =
+ * [Wh[n] (heads*f) | 0-pad | s_src[n] (heads) | 0-pad], both parts 16-B aligned.
  */
 int gat_table_layout(int heads, int f, int* ld, int* s_off);
 
@@ -56,35 +57,42 @@ int gat_table_layout(int heads, int f, int* ld, int* s_off);
  * Dense head projection with fused attention scores.
  * Replaces GAT.py:42-52 (per head h: ws[h](x), attentions1[h](.), attentions2[h](.),
  * then stack/transpose).
- *   x      [n, fin]      row-major
+ *   x      [n, fin]       row-major
  *   w      [heads*f, fin] = cat_h ws[h].weight          (GAT.py:20)
  *   b      [heads*f]      = cat_h ws[h].bias
  *   a_src  [heads*f]      = cat_h attentions1[h].weight  (GAT.py:21, source term)
  *   c_src  [heads]        = cat_h attentions1[h].bias
  *   a_dst, c_dst          = the same for attentions2     (GAT.py:22, target term)
- * Writes table rows [0, n) (layout above) and s_dst [n, heads].
+ * Writes, for rows [0, n):
+ *   wh     [n, ld_wh]  Wh = x W^T + b, head-major (column h*f + k): the
+ *                      reference's stack/transpose [N,H,F] view (GAT.py:49-50)
+ *                      made contiguous; columns [heads*f, round_up(heads*f, 4))
+ *                      zeroed; ld_wh % 4 == 0, ld_wh >= round_up(heads*f, 4)
+ *   s_src  [n, ld_s]   Wh_h . a_src_h + c_src_h   (ld_s >= heads)
+ *   s_dst  [n, heads]  Wh_h . a_dst_h + c_dst_h
  */
 int gat_project(const float* x, int n, int fin, const float* w, const float* b,
                 const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,
-                int heads, int f, float* table, int ld, int s_off, float* s_dst, void* stream);
+                int heads, int f, float* wh, int ld_wh, float* s_src, int ld_s, float* s_dst,
+                void* stream);
 
 /*
  * Fused per-edge score + LeakyReLU + segmented softmax + attention-weighted
  * aggregation + concat/head-mean + bias over target rows [row_begin, row_end).
  * Replaces GAT.py:53-67 (PyG propagate/__collect__, message, utils.softmax,
  * aggregate aggr='add') and GAT.py:54 (+ bias).
- *   rowptr/col  CSR by target (gat_csr_build); col holds table row ids
- *   table       node table (gat_project / an all-gathered copy)
- *   s_dst       [rows, heads], indexed by target row
- *   bias        [heads*f] if concat else [f]
- *   out         [rows, heads*f] if concat else [rows, f], indexed by target row
- *   lse         optional [rows, heads] = max + log(sum exp) per (row, head)
- *               (for the backward pass); may be NULL
+ *   rowptr/col   CSR by target (gat_csr_build); col holds source row ids into wh/s_src
+ *   wh, s_src    as written by gat_project (or an all-gathered copy)
+ *   s_dst        [rows, heads], indexed by target row
+ *   bias         [heads*f] if concat else [f]
+ *   out          [rows, heads*f] if concat else [rows, f], indexed by target row
+ *   lse          optional [rows, heads] = max + log(sum exp) per (row, head)
+ *                (for the backward pass); may be NULL
  */
 int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row_end,
-                       const float* table, int ld, int s_off, const float* s_dst, int heads,
-                       int f, int concat, float negative_slope, const float* bias, float* out,
-                       float* lse, void* stream);
+                       const float* wh, int ld_wh, const float* s_src, int ld_s,
+                       const float* s_dst, int heads, int f, int concat, float negative_slope,
+                       const float* bias, float* out, float* lse, void* stream);
 
 /* Workspace bytes gat_csr_build needs for (num_edges, num_nodes). */
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);

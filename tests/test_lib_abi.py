@@ -48,15 +48,19 @@ def test_argument_validation_without_gpu():
     from atmlgraphattentionnetworks_amd import _lib
     lib = _lib.load()
     # bad sizes are rejected before anything touches a device
-    assert lib.gat_project(None, -1, 4, None, None, None, None, None, None, 2, 2, None, 8, 4,
-                           None, None) == _lib.GAT_EINVAL
-    assert lib.gat_project(None, 10, 4, None, None, None, None, None, None, 65, 2, None, 200,
-                           132, None, None) == _lib.GAT_EUNSUPPORTED
-    assert lib.gat_edge_aggregate(None, None, 0, 10, None, 8, 2, None, 2, 2, 1, 0.2, None, None,
-                                  None, None) == _lib.GAT_EINVAL  # s_off < H*F
+    assert lib.gat_project(None, -1, 4, None, None, None, None, None, None, 2, 2, None, 4, None,
+                           2, None, None) == _lib.GAT_EINVAL
+    assert lib.gat_project(None, 10, 4, None, None, None, None, None, None, 65, 2, None, 132,
+                           None, 65, None, None) == _lib.GAT_EUNSUPPORTED
+    assert lib.gat_project(None, 10, 4, None, None, None, None, None, None, 2, 3, None, 6,
+                           None, 2, None, None) == _lib.GAT_EINVAL  # ld_wh not 16-B aligned
+    assert lib.gat_edge_aggregate(None, None, 0, 10, None, 2, None, 2, None, 2, 2, 1, 0.2, None,
+                                  None, None, None) == _lib.GAT_EINVAL  # ld_wh < H*F
+    assert lib.gat_edge_aggregate(None, None, 0, 10, None, 4, None, 1, None, 2, 2, 1, 0.2, None,
+                                  None, None, None) == _lib.GAT_EINVAL  # ld_s < H
     # zero rows: nothing to launch
-    assert lib.gat_edge_aggregate(None, None, 5, 5, None, 8, 4, None, 2, 2, 1, 0.2, None, None,
-                                  None, None) == _lib.GAT_OK
+    assert lib.gat_edge_aggregate(None, None, 5, 5, None, 4, None, 2, None, 2, 2, 1, 0.2, None,
+                                  None, None, None) == _lib.GAT_OK
     with pytest.raises(_lib.GatLibraryError):
         _lib.check(_lib.GAT_EUNSUPPORTED, "x")
 

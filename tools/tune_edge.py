@@ -59,7 +59,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
-    from atmlgraphattentionnetworks_amd.layer import edge_aggregate, project
+    from atmlgraphattentionnetworks_amd.layer import alloc_table, edge_aggregate, project
     from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
     from bench import edge_kernel_bytes
 
@@ -96,7 +96,7 @@ def main():
         for r in range(args.rounds):
             for name, env in PROJ_VARIANTS.items():
                 set_env(env)
-                t2, s2 = torch.empty_like(table), torch.empty_like(s_dst)
+                t2 = alloc_table(n, H, F, dev); s2 = torch.empty_like(s_dst)
                 pres[name].append(time_fn(lambda: project(x, pp, H, F, table=t2, s_dst=s2),
                                           args.iters))
                 pouts[name] = (t2, s2)
@@ -104,7 +104,7 @@ def main():
             summary["proj_" + name] = {
                 "median_ms": statistics.median(ts), "min_ms": min(ts),
                 "max_abs_diff_vs_generic": max(
-                    float((pouts[name][0] - pouts["generic"][0]).abs().max()),
+                    float((pouts[name][0].wh - pouts["generic"][0].wh).abs().max()),
                     float((pouts[name][1] - pouts["generic"][1]).abs().max()))}
     print(json.dumps({"workload": args.workload, "N": n, "E'": csr.num_edges,
                       "alg_bytes": alg, "results": summary}, indent=1))
