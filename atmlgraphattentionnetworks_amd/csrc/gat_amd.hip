@@ -107,9 +107,12 @@ __global__ __launch_bounds__(256) void k_project(
             float wv[WB];
 #pragma unroll
             for (int q = 0; q < WB; ++q) {
+                // unconditional load from a clamped address times a 0/1 mask:
+                // a guarded load compiles to a branch + vmcnt(0) per element
                 const int idx = tid + (b0 + q) * 256;
                 const int nn = idx / BK, gk = k0 + idx % BK;
-                wv[q] = (nn < HF && gk < fin) ? W[(size_t)nn * fin + gk] : 0.f;
+                wv[q] = W[(size_t)min(nn, HF - 1) * fin + min(gk, fin - 1)] *
+                        ((nn < HF && gk < fin) ? 1.f : 0.f);
             }
 #pragma unroll
             for (int q = 0; q < WB; ++q) {
@@ -120,8 +123,10 @@ __global__ __launch_bounds__(256) void k_project(
         float xa[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
+            // value used unconditionally (x 0/1 mask), so the load is never
+            // sunk into a branch with its own vmcnt(0); padded k: x * 0
             const int kk = k0 + 4 * s + kq;
-            xa[s] = kk < fin ? xr[kk] * xs : 0.f;
+            xa[s] = xr[min(kk, fin - 1)] * (kk < fin ? xs : 0.f);
         }
         __syncthreads();
         const int ksteps = min(KS, (fin - k0 + 3) / 4);
@@ -393,19 +398,28 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 //
 // Lane c of a group owns the float4 columns [4c, 4c+4) of the row — all in
 // head h = 4c / F — and runs that head's online softmax in registers, so the
-// hot loop has no LDS traffic, no barriers and no cross-lane reductions.
-// Per chunk of U in-edges: one coalesced col load, U broadcasts by shuffle,
-// then U independent (s_src, Wh float4) gathers in flight per lane, one
-// rescale per chunk.  Head mean (concat=False, F/4 a power of two) is an
-// xor-butterfly over the group.
+// hot loop has no LDS traffic, no barriers and no cross-lane reductions
+// beyond the score's.  Per chunk of U in-edges: one coalesced col load, U
+// broadcasts by shuffle, then U independent Wh float4 gathers in flight per
+// lane and one rescale per chunk.
+// FUSED: the source score s_src[j,h] = Wh[j,h].a1_h + c1_h is recomputed from
+// the gathered row (4 FMAs + an xor-add over the head's F/4 lanes) instead
+// of being gathered — one VMEM instruction and up to a cache line less per
+// edge.  Softmax runs in log2 units: e' = LeakyReLU(z) * log2(e), p = 2^(e'-m').
+// Head mean (concat=False, F/4 a power of two) is an xor-butterfly over the
+// group.
 // ---------------------------------------------------------------------------
-template <int G, int U, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_edge_grp(
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+template <int G, int U, bool FUSED>
+__global__ __launch_bounds__(256) void k_edge_grp(
     const int* __restrict__ rowptr, const int* __restrict__ col, int row_begin, int row_end,
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
-    const float* __restrict__ s_dst,
-    int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
-    float* __restrict__ out, int ld_out, float* __restrict__ lse) {
+    const float* __restrict__ a_src, const float* __restrict__ c_src,
+    const float* __restrict__ s_dst, int H, int F, int HF, int concat, float slope,
+    const float* __restrict__ bias, float* __restrict__ out, int ld_out,
+    float* __restrict__ lse) {
     constexpr int CL = (U + G - 1) / G;  // col values held per lane per chunk
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
@@ -415,43 +429,56 @@ __global__ __launch_bounds__(256, MINW) void k_edge_grp(
     const bool c_ok = 4 * c < HF;
     const int coff = c_ok ? 4 * c : 0;
     const int h = coff / F;
+    f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+    float c1 = 0.f;
+    if constexpr (FUSED) {
+        if (c_ok) a4 = *reinterpret_cast<const f32x4*>(a_src + coff);
+        c1 = c_src[h];
+    }
     const int e0 = rowptr[r], e1 = rowptr[r + 1];
     const float sd = s_dst[(size_t)r * H + h];
-    float m = -INFINITY, l = 0.f;
+    float m = -INFINITY, l = 0.f;  // running max in log2 units
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 
     for (int k = e0; k < e1; k += U) {
         const int nk = min(U, e1 - k);
         int cv[CL];
 #pragma unroll
-        for (int t = 0; t < CL; ++t) {
-            const int idx = c + t * G;
-            cv[t] = idx < nk ? col[k + idx] : -1;
-        }
+        for (int t = 0; t < CL; ++t) cv[t] = col[k + min(c + t * G, nk - 1)];  // unconditional
         int j[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) j[u] = __shfl(cv[u / G], gbase + (u % G));
-        float s[U];
         f32x4 v[U];
+        float s[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const size_t jj = (size_t)(j[u] >= 0 ? j[u] : j[0]);
-            s[u] = Ss[jj * ld_s + h];
-            v[u] = *reinterpret_cast<const f32x4*>(Wh + jj * ld_wh + coff);
+            v[u] = *reinterpret_cast<const f32x4*>(Wh + (size_t)j[u] * ld_wh + coff);
+            if constexpr (!FUSED) s[u] = Ss[(size_t)j[u] * ld_s + h];
+        }
+        if constexpr (FUSED) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                s[u] = fmaf(v[u].w, a4.w, fmaf(v[u].z, a4.z, fmaf(v[u].y, a4.y, v[u].x * a4.x)));
+            for (int off = 1; off < F / 4; off <<= 1)
+#pragma unroll
+                for (int u = 0; u < U; ++u) s[u] += __shfl_xor(s[u], off);
+#pragma unroll
+            for (int u = 0; u < U; ++u) s[u] += c1;
         }
         float emax = -INFINITY;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            s[u] = j[u] >= 0 ? leaky(sd + s[u], slope) : -INFINITY;
+            const float z = sd + s[u];
+            s[u] = u < nk ? fmaxf(z, z * slope) * kLog2e : -INFINITY;  // slope in [0, 1]
             emax = fmaxf(emax, s[u]);
         }
         const float m_new = fmaxf(m, emax);
-        const float scale = expf(m - m_new);
+        const float scale = __builtin_amdgcn_exp2f(m - m_new);
         l *= scale;
         acc *= scale;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const float p = expf(s[u] - m_new);
+            const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
             l += p;
             acc += p * v[u];
         }
@@ -460,7 +487,8 @@ __global__ __launch_bounds__(256, MINW) void k_edge_grp(
 
     const float inv = 1.f / (l + 1e-16f);
     f32x4 y = acc * inv;
-    if (lse != nullptr && c_ok && (coff % F) == 0) lse[(size_t)r * H + h] = m + logf(l);
+    if (lse != nullptr && c_ok && (coff % F) == 0)
+        lse[(size_t)r * H + h] = (m + log2f(l)) * kLn2;  // natural-log units
     if (concat) {
         if (c_ok) {
             const f32x4 b = *reinterpret_cast<const f32x4*>(bias + coff);
@@ -624,33 +652,41 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
 
 int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row_end,
                        const float* wh, int ld_wh, const float* s_src, int ld_s,
-                       const float* s_dst, int heads, int f, int concat, float negative_slope,
-                       const float* bias, float* out, float* lse, void* stream) {
+                       const float* a_src, const float* c_src, const float* s_dst, int heads,
+                       int f, int concat, float negative_slope, const float* bias, float* out,
+                       float* lse, void* stream) {
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
-    if (ld_wh < round_up4(hf) || (ld_wh & 3) || ld_s < heads) return GAT_EINVAL;
+    if (ld_wh < round_up4(hf) || (ld_wh & 3)) return GAT_EINVAL;
+    if (s_src != nullptr && ld_s < heads) return GAT_EINVAL;
+    const bool have_a = a_src != nullptr && c_src != nullptr;
+    if (s_src == nullptr && !have_a) return GAT_EINVAL;
     const int rows = row_end - row_begin;
     if (rows == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
     const int ld_out = concat ? hf : f;
     const int g = next_pow2((hf + 3) / 4);
     const bool pow2_f4 = (f % 4 == 0) && next_pow2(f / 4) == f / 4;
-    const bool grp_ok = (f % 4 == 0) && (concat || pow2_f4);
-    if (grp_ok && kernel_choice("GAT_EDGE_KERNEL", "group", "generic")) {
+    const bool slope_ok = negative_slope >= 0.f && negative_slope <= 1.f;
+    const bool grp_ok = (f % 4 == 0) && (concat || pow2_f4) && slope_ok;
+    // fused source score: needs the head's lanes to form an aligned power-of-two block
+    bool fused = grp_ok && pow2_f4 && have_a;
+    if (fused && s_src != nullptr) fused = kernel_choice("GAT_EDGE_SCORE", "fused", "gather");
+    if (s_src == nullptr && !fused) return GAT_EUNSUPPORTED;
+    if (grp_ok && (s_src == nullptr || kernel_choice("GAT_EDGE_KERNEL", "group", "generic"))) {
         const int u = edge_unroll();
-        const bool occ8 = std::getenv("GAT_EDGE_OCC8") != nullptr;
         const long long threads = (long long)rows * g;
         const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
 #define GAT_GRP_LAUNCH(G, UU)                                                                  \
-    if (occ8)                                                                                  \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, 8>), grid, block, 0, st, rowptr, col, row_begin, \
-                           row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,             \
-                           negative_slope, bias, out, ld_out, lse);                            \
+    if (fused)                                                                                 \
+        hipLaunchKernelGGL((k_edge_grp<G, UU, true>), grid, block, 0, st, rowptr, col,         \
+                           row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,    \
+                           heads, f, hf, concat, negative_slope, bias, out, ld_out, lse);      \
     else                                                                                       \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, 1>), grid, block, 0, st, rowptr, col, row_begin, \
-                           row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,             \
-                           negative_slope, bias, out, ld_out, lse)
+        hipLaunchKernelGGL((k_edge_grp<G, UU, false>), grid, block, 0, st, rowptr, col,        \
+                           row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,    \
+                           heads, f, hf, concat, negative_slope, bias, out, ld_out, lse)
 #define GAT_GRP_U(G)                            \
     if (u == 4) { GAT_GRP_LAUNCH(G, 4); }       \
     else if (u == 16) { GAT_GRP_LAUNCH(G, 16); } \

@@ -78,9 +78,10 @@ class HipOps:
         return project(x, pp, heads, f, table=table, s_dst=s_dst)
 
     @staticmethod
-    def edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope, out):
+    def edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope, out, pp=None):
         from .layer import edge_aggregate
-        return edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope, out=out)
+        return edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope, out=out,
+                              pp=pp)
 
 
 class ShardedGAT:
@@ -143,7 +144,7 @@ class ShardedGAT:
         s_dst = self.s_dst_full if self.exchange == "allgather" else \
             self.s_dst_full[self.r0:self.r1]
         return self.ops.edge_aggregate(self.local, self.table, s_dst, self.heads, self.f,
-                                       self.concat, self.bias, 0.2, self.out)
+                                       self.concat, self.bias, 0.2, self.out, pp=self.pp)
 
     def forward(self, x):
         """x: this rank's rows [n_local, Fin] (allgather) or all rows (replicate)."""

@@ -114,8 +114,11 @@ def project(x: torch.Tensor, pp: PackedParams, heads: int, f: int,
 def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: int,
                    concat: bool, bias: torch.Tensor, negative_slope: float = 0.2,
                    row_begin: int = 0, row_end: Optional[int] = None,
-                   out: Optional[torch.Tensor] = None, lse: Optional[torch.Tensor] = None):
-    """``gat_edge_aggregate`` over target rows [row_begin, row_end)."""
+                   out: Optional[torch.Tensor] = None, lse: Optional[torch.Tensor] = None,
+                   pp: Optional[PackedParams] = None):
+    """``gat_edge_aggregate`` over target rows [row_begin, row_end).  With
+    ``pp`` the library may recompute the source score from the gathered Wh
+    row (a_src/c_src) instead of gathering s_src."""
     lib = _lib.load()
     rows = csr.num_nodes if row_end is None else row_end
     width = heads * f if concat else f
@@ -123,9 +126,11 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
         out = torch.empty(rows, width, dtype=torch.float32, device=table.wh.device)
     _lib.check(lib.gat_edge_aggregate(
         csr.rowptr.data_ptr(), csr.col.data_ptr(), row_begin, rows, table.wh.data_ptr(),
-        table.ld_wh, table.s_src.data_ptr(), table.ld_s, s_dst.data_ptr(), heads, f,
-        int(concat), float(negative_slope), bias.data_ptr(), out.data_ptr(),
-        0 if lse is None else lse.data_ptr(), _stream(table.wh.device)), "gat_edge_aggregate")
+        table.ld_wh, table.s_src.data_ptr(), table.ld_s,
+        0 if pp is None else pp.a_src.data_ptr(), 0 if pp is None else pp.c_src.data_ptr(),
+        s_dst.data_ptr(), heads, f, int(concat), float(negative_slope), bias.data_ptr(),
+        out.data_ptr(), 0 if lse is None else lse.data_ptr(), _stream(table.wh.device)),
+        "gat_edge_aggregate")
     return out
 
 
@@ -133,7 +138,7 @@ def gat_forward(x: torch.Tensor, csr: CSRGraph, pp: PackedParams, bias: torch.Te
                 heads: int, f: int, concat: bool, negative_slope: float = 0.2) -> torch.Tensor:
     """Layer forward on prepared inputs: projection + edge kernel (2 launches)."""
     table, s_dst = project(x, pp, heads, f)
-    return edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope)
+    return edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope, pp=pp)
 
 
 def _check_x(x: torch.Tensor, in_channels: int) -> torch.Tensor:

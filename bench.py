@@ -158,13 +158,13 @@ def main():
                           device=dev)
         for _ in range(5):
             edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat, layer.bias,
-                           out=out)
+                           out=out, pp=pp)
         stream = torch.cuda.current_stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record(stream)
         for _ in range(args.edge_iters):
             edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat, layer.bias,
-                           out=out)
+                           out=out, pp=pp)
         ev1.record(stream)
         ev1.synchronize()
         edge_ms = ev0.elapsed_time(ev1) / args.edge_iters

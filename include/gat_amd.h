@@ -82,17 +82,26 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
  * Replaces GAT.py:53-67 (PyG propagate/__collect__, message, utils.softmax,
  * aggregate aggr='add') and GAT.py:54 (+ bias).
  *   rowptr/col   CSR by target (gat_csr_build); col holds source row ids into wh/s_src
- *   wh, s_src    as written by gat_project (or an all-gathered copy)
+ *   wh           as written by gat_project (or an all-gathered copy)
+ *   s_src, ld_s  the source term per node, as written by gat_project; may be NULL
+ *                when a_src/c_src are given
+ *   a_src, c_src the attentions1 parameters (gat_project's a_src/c_src); when given,
+ *                the library may recompute s_src[j] from the gathered Wh[j] row
+ *                instead of gathering it (same value up to fp32 rounding); may be
+ *                NULL when s_src is given
  *   s_dst        [rows, heads], indexed by target row
  *   bias         [heads*f] if concat else [f]
  *   out          [rows, heads*f] if concat else [rows, f], indexed by target row
  *   lse          optional [rows, heads] = max + log(sum exp) per (row, head)
- *                (for the backward pass); may be NULL
+ *                (natural log; for the backward pass); may be NULL
+ * GAT_EUNSUPPORTED if s_src is NULL and the shape needs it (f % 4 != 0, or
+ * f/4 not a power of two, or negative_slope outside [0, 1]).
  */
 int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row_end,
                        const float* wh, int ld_wh, const float* s_src, int ld_s,
-                       const float* s_dst, int heads, int f, int concat, float negative_slope,
-                       const float* bias, float* out, float* lse, void* stream);
+                       const float* a_src, const float* c_src, const float* s_dst, int heads,
+                       int f, int concat, float negative_slope, const float* bias, float* out,
+                       float* lse, void* stream);
 
 /* Workspace bytes gat_csr_build needs for (num_edges, num_nodes). */
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);

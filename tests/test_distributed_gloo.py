@@ -41,7 +41,7 @@ class CpuOps:
         s_dst[:] = (v * pp.a_dst.view(heads, f)).sum(-1) + pp.c_dst
 
     @staticmethod
-    def edge_aggregate(csr, table, s_dst, heads, f, concat, bias, slope, out):
+    def edge_aggregate(csr, table, s_dst, heads, f, concat, bias, slope, out, pp=None):
         hf = heads * f
         rp = csr.rowptr.long()
         deg = rp[1:] - rp[:-1]

@@ -29,12 +29,13 @@ VARIANTS = {
     "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds"},
     "fast_u4": {"GAT_EDGE_U": "4"},
     "fast_u16": {"GAT_EDGE_U": "16"},
+    "gather_score": {"GAT_EDGE_SCORE": "gather"},
 }
 
 
 @pytest.fixture(params=list(VARIANTS))
 def variant(request, monkeypatch):
-    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U"):
+    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)

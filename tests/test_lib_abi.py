@@ -54,13 +54,16 @@ def test_argument_validation_without_gpu():
                            None, 65, None, None) == _lib.GAT_EUNSUPPORTED
     assert lib.gat_project(None, 10, 4, None, None, None, None, None, None, 2, 3, None, 6,
                            None, 2, None, None) == _lib.GAT_EINVAL  # ld_wh not 16-B aligned
-    assert lib.gat_edge_aggregate(None, None, 0, 10, None, 2, None, 2, None, 2, 2, 1, 0.2, None,
-                                  None, None, None) == _lib.GAT_EINVAL  # ld_wh < H*F
-    assert lib.gat_edge_aggregate(None, None, 0, 10, None, 4, None, 1, None, 2, 2, 1, 0.2, None,
-                                  None, None, None) == _lib.GAT_EINVAL  # ld_s < H
+    E = lib.gat_edge_aggregate
+    assert E(None, None, 0, 10, None, 2, 1, 2, None, None, None, 2, 2, 1, 0.2, None, None, None,
+             None) == _lib.GAT_EINVAL  # ld_wh < H*F
+    assert E(None, None, 0, 10, None, 4, 1, 1, None, None, None, 2, 2, 1, 0.2, None, None, None,
+             None) == _lib.GAT_EINVAL  # ld_s < H
+    assert E(None, None, 0, 10, None, 4, None, 2, None, None, None, 2, 2, 1, 0.2, None, None,
+             None, None) == _lib.GAT_EINVAL  # neither s_src nor (a_src, c_src)
     # zero rows: nothing to launch
-    assert lib.gat_edge_aggregate(None, None, 5, 5, None, 4, None, 2, None, 2, 2, 1, 0.2, None,
-                                  None, None, None) == _lib.GAT_OK
+    assert E(None, None, 5, 5, None, 4, 1, 2, None, None, None, 2, 2, 1, 0.2, None, None, None,
+             None) == _lib.GAT_OK
     with pytest.raises(_lib.GatLibraryError):
         _lib.check(_lib.GAT_EUNSUPPORTED, "x")
 

@@ -47,7 +47,7 @@ def main():
         for _ in range(args.iters):
             project(x, pp, w.heads, w.out_channels, table=table, s_dst=s_dst)
             out = edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat,
-                                 layer.bias, out=out)
+                                 layer.bias, out=out, pp=pp)
         torch.cuda.synchronize()
     print(f"pmc_run done: {args.workload} N={x.size(0)} E'={csr.num_edges}")
 

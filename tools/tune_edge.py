@@ -17,17 +17,16 @@ import torch  # noqa: E402
 
 EDGE_VARIANTS = {
     "generic": {"GAT_EDGE_KERNEL": "generic"},
-    "grp_u4": {"GAT_EDGE_U": "4"},
-    "grp_u8": {"GAT_EDGE_U": "8"},
-    "grp_u16": {"GAT_EDGE_U": "16"},
-    "grp_u8_occ8": {"GAT_EDGE_U": "8", "GAT_EDGE_OCC8": "1"},
-    "grp_u4_occ8": {"GAT_EDGE_U": "4", "GAT_EDGE_OCC8": "1"},
+    "grp_gather_u8": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_U": "8"},
+    "grp_fused_u4": {"GAT_EDGE_U": "4"},
+    "grp_fused_u8": {"GAT_EDGE_U": "8"},
+    "grp_fused_u16": {"GAT_EDGE_U": "16"},
 }
 PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "shfl": {}}
 
 
 def set_env(d):
-    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_OCC8"):
+    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE"):
         os.environ.pop(k, None)
     os.environ.update(d)
 
@@ -83,7 +82,7 @@ def main():
                 set_env(env)
                 out = torch.empty(n, H * F if w.concat else F, device=dev)
                 res[name].append(time_fn(lambda: edge_aggregate(
-                    csr, table, s_dst, H, F, w.concat, layer.bias, out=out), args.iters))
+                    csr, table, s_dst, H, F, w.concat, layer.bias, out=out, pp=pp), args.iters))
                 outs[name] = out
         ref = outs["generic"]
         alg = edge_kernel_bytes(n, csr.num_edges, H, F, w.concat)
