@@ -245,6 +245,143 @@ __global__ __launch_bounds__(256) void k_project(
 }
 
 // ---------------------------------------------------------------------------
+// Cross-lane sums with DPP (a VALU modifier: no LDS round trip).  Sums over
+// aligned groups of w lanes, w a power of two <= 16, within each 16-lane row:
+// quad_perm [1,0,3,2] (xor 1), quad_perm [2,3,0,1] (xor 2), then
+// row_half_mirror / row_mirror, which pair each quad (8-group) with the other
+// one of its 8-group (16-row) — enough for a sum.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float group_sum16(float v, int w) {
+    if (w >= 2) v += dpp_mov<0xB1>(v);
+    if (w >= 4) v += dpp_mov<0x4E>(v);
+    if (w >= 8) v += dpp_mov<0x141>(v);
+    if (w >= 16) v += dpp_mov<0x140>(v);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// Projection, direct-load variant (F a power of two): one wave owns 16 node
+// rows x TW column tiles (TW*16 columns, whole heads), so a PPI-shape layer
+// runs 2x the waves of the LDS-tiled kernel.  MFMA A/B fragments are loaded
+// straight to registers — X rows once, W (a few KB) from L1/L2 — in K chunks
+// of 16/TW k-steps with the next chunk in flight during the current MFMAs; no
+// LDS, no barriers.  Epilogue parameters are loaded up front; the score dot
+// products are summed across the head's lanes with DPP.
+// ---------------------------------------------------------------------------
+template <int TW>
+__global__ __launch_bounds__(256) void k_project_direct(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, int col_groups, float* __restrict__ Wh, int ld_wh,
+    float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst) {
+    constexpr int KC = TW >= 16 ? 1 : 16 / TW;  // k-steps (of 4) per chunk: ~KC*(1+TW) loads
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int rg = wave / col_groups, cg = wave % col_groups;
+    const int row0 = rg * 16;
+    if (row0 >= n) return;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int hfp = round_up4(HF);
+    const float* xr = X + (size_t)min(row0 + cl, n - 1) * fin;
+    const float* wr[TW];
+    float wm[TW], bb[TW], w1[TW], w2[TW];
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+        const int cc = (cg * TW + t) * 16 + cl;
+        const bool ok = cc < HF;
+        wr[t] = W + (size_t)min(cc, HF - 1) * fin;
+        wm[t] = ok ? 1.f : 0.f;
+        bb[t] = bW[min(cc, HF - 1)] * wm[t];  // epilogue parameters, loaded up front
+        w1[t] = a1[min(cc, HF - 1)] * wm[t];
+        w2[t] = a2[min(cc, HF - 1)] * wm[t];
+    }
+    f32x4 acc[TW];
+#pragma unroll
+    for (int t = 0; t < TW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // loads are unconditional (clamped address x 0/1 mask): a guarded load
+    // compiles to a branch + vmcnt(0) per element
+    float xa[KC], wa[KC][TW];
+    auto load_chunk = [&](int k0, float (&xs)[KC], float (&ws)[KC][TW]) {
+#pragma unroll
+        for (int s = 0; s < KC; ++s) {
+            const int kk = k0 + 4 * s + kq;
+            const float km = kk < fin ? 1.f : 0.f;
+            const int kc = min(kk, fin - 1);
+            xs[s] = xr[kc] * km;
+#pragma unroll
+            for (int t = 0; t < TW; ++t) ws[s][t] = wr[t][kc] * wm[t];
+        }
+    };
+    if (fin > 0) load_chunk(0, xa, wa);
+    for (int k0 = 0; k0 < fin; k0 += 4 * KC) {
+        const bool more = k0 + 4 * KC < fin;
+        float xb[KC], wb[KC][TW];
+        if (more) load_chunk(k0 + 4 * KC, xb, wb);
+        const int steps = min(KC, (fin - k0 + 3) / 4);
+#pragma unroll
+        for (int s = 0; s < KC; ++s) {
+            if (s < steps) {  // wave-uniform
+#pragma unroll
+                for (int t = 0; t < TW; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], wa[s][t], acc[t], 0, 0, 0);
+            }
+        }
+        if (more) {
+#pragma unroll
+            for (int s = 0; s < KC; ++s) {
+                xa[s] = xb[s];
+#pragma unroll
+                for (int t = 0; t < TW; ++t) wa[s][t] = wb[s][t];
+            }
+        }
+    }
+
+    // accumulator map: column (cg*TW + t)*16 + cl, rows (lane >> 4) * 4 + i
+    float p1[4] = {0.f, 0.f, 0.f, 0.f}, p2[4] = {0.f, 0.f, 0.f, 0.f};
+    const int tph = F >= 16 ? F / 16 : 1;  // tiles per head
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+        const int cc = (cg * TW + t) * 16 + cl;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float v = acc[t][i] + bb[t];  // Linear bias inside Wh (GAT.py:43)
+            const int rr = row0 + (lane >> 4) * 4 + i;
+            if (rr < n && cc < hfp) Wh[(size_t)rr * ld_wh + cc] = v;
+            p1[i] = fmaf(v, w1[t], p1[i]);
+            p2[i] = fmaf(v, w2[t], p2[i]);
+        }
+        if ((t + 1) % tph == 0) {  // p1/p2 now hold this lane's share of a whole head
+            const int gw = F < 16 ? F : 16;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                p1[i] = group_sum16(p1[i], gw);
+                p2[i] = group_sum16(p2[i], gw);
+            }
+            const int h = cc / F;
+            if ((cl & (gw - 1)) == 0 && h < H) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = row0 + (lane >> 4) * 4 + i;
+                    if (rr >= n) continue;
+                    Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
+                    s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) p1[i] = p2[i] = 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Edge kernel: one wavefront (= one 64-thread workgroup) per target row.
 //
 // For each chunk of C in-edges of row r:
@@ -440,11 +577,16 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     float m = -INFINITY, l = 0.f;  // running max in log2 units
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 
+    // col indices are software-pipelined: chunk k+U's are in flight while
+    // chunk k gathers (loads unconditional, clamped to the row's last edge)
+    int cv[CL];
+#pragma unroll
+    for (int t = 0; t < CL; ++t) cv[t] = col[min(e0 + c + t * G, e1 - 1)];
     for (int k = e0; k < e1; k += U) {
         const int nk = min(U, e1 - k);
-        int cv[CL];
+        int cn[CL];
 #pragma unroll
-        for (int t = 0; t < CL; ++t) cv[t] = col[k + min(c + t * G, nk - 1)];  // unconditional
+        for (int t = 0; t < CL; ++t) cn[t] = col[min(k + U + c + t * G, e1 - 1)];
         int j[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) j[u] = __shfl(cv[u / G], gbase + (u % G));
@@ -459,9 +601,14 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 s[u] = fmaf(v[u].w, a4.w, fmaf(v[u].z, a4.z, fmaf(v[u].y, a4.y, v[u].x * a4.x)));
-            for (int off = 1; off < F / 4; off <<= 1)
+            if (F <= 64) {  // the head's F/4 lanes sit in one 16-lane DPP row
 #pragma unroll
-                for (int u = 0; u < U; ++u) s[u] += __shfl_xor(s[u], off);
+                for (int u = 0; u < U; ++u) s[u] = group_sum16(s[u], F / 4);
+            } else {
+                for (int off = 1; off < F / 4; off <<= 1)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) s[u] += __shfl_xor(s[u], off);
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u) s[u] += c1;
         }
@@ -483,6 +630,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
             acc += p * v[u];
         }
         m = m_new;
+#pragma unroll
+        for (int t = 0; t < CL; ++t) cv[t] = cn[t];
     }
 
     const float inv = 1.f / (l + 1e-16f);
@@ -626,8 +775,32 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
     const int nt = (hf + 15) / 16;
+    // GAT_PROJ_KERNEL (A/B knob): "direct" (default where F is a power of two),
+    // "tiled" (LDS-tiled, shuffle epilogue), "lds" (LDS-tiled, LDS epilogue)
+    const char* pk = std::getenv("GAT_PROJ_KERNEL");
+    const bool pow2_f = next_pow2(f) == f;
+    if (pow2_f && (pk == nullptr || std::strcmp(pk, "direct") == 0)) {
+        int tw = nt < 2 ? nt : 2;
+        if (f / 16 > tw) tw = f / 16;
+        const int cgroups = (nt + tw - 1) / tw;
+        const long long waves = (long long)((n + 15) / 16) * cgroups;
+        const dim3 gd((unsigned)((waves + 3) / 4)), bd(256);
+#define GAT_PD(TW)                                                                             \
+    hipLaunchKernelGGL((k_project_direct<TW>), gd, bd, 0, st, x, n, fin, w, b, a_src, c_src,    \
+                       a_dst, c_dst, heads, f, hf, cgroups, wh, ld_wh, s_src, ld_s, s_dst)
+        switch (tw) {
+            case 1: GAT_PD(1); break;
+            case 2: GAT_PD(2); break;
+            case 4: GAT_PD(4); break;
+            case 8: GAT_PD(8); break;
+            case 16: GAT_PD(16); break;
+            default: return GAT_EUNSUPPORTED;
+        }
+#undef GAT_PD
+        return status_of(hipGetLastError());
+    }
     const bool shfl = ((f <= 16 && 16 % f == 0) || (f % 16 == 0)) &&
-                      kernel_choice("GAT_PROJ_KERNEL", "shfl", "lds");
+                      !(pk != nullptr && std::strcmp(pk, "lds") == 0);
 #define GAT_PROJ_CASE(NT)                                                                   \
     case NT:                                                                                \
         if (shfl)                                                                           \

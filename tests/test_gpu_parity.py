@@ -30,6 +30,7 @@ VARIANTS = {
     "fast_u4": {"GAT_EDGE_U": "4"},
     "fast_u16": {"GAT_EDGE_U": "16"},
     "gather_score": {"GAT_EDGE_SCORE": "gather"},
+    "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
 }
 
 

@@ -22,7 +22,7 @@ EDGE_VARIANTS = {
     "grp_fused_u8": {"GAT_EDGE_U": "8"},
     "grp_fused_u16": {"GAT_EDGE_U": "16"},
 }
-PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "shfl": {}}
+PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "tiled": {"GAT_PROJ_KERNEL": "tiled"}, "direct": {}}
 
 
 def set_env(d):
