@@ -382,6 +382,109 @@ __global__ __launch_bounds__(256) void k_project_direct(
 }
 
 // ---------------------------------------------------------------------------
+// Projection, whole-K variant (fin <= 128): the workgroup's 64 X rows are one
+// contiguous 64*fin*4-byte chunk of HBM, and W [HF, fin] is contiguous too, so
+// both are staged into LDS with fully coalesced float4 loads (16x fewer
+// memory requests than per-row fragment loads) and the MFMAs read their A/B
+// fragments from LDS.  The output tile goes back through LDS so that Wh rows
+// leave as coalesced float4 stores and each (row, head) score is one short
+// dot product per thread.  Two barriers per workgroup, no K loop.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void k_project_wk(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh,
+    float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst) {
+    constexpr int BM = 64, BN = NT * 16;
+    constexpr int OS = BN + 4;  // output-tile stride: float4-aligned rows, no write conflicts
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int row0 = blockIdx.x * BM;
+    const int rows = min(BM, n - row0);
+    const int xs_n = round_up4(BM * fin);  // X tile floats (16-B aligned W tile after it)
+    float* Xs = smem;
+    float* Ws = smem + xs_n;
+
+    // X rows [row0, row0+rows): one contiguous chunk; row0*fin*4 = 256*b*fin bytes is 16-B aligned
+    {
+        const float* xg = X + (size_t)row0 * fin;
+        const int cnt = rows * fin, cnt4 = cnt & ~3;
+        for (int i = tid * 4; i < cnt4; i += 1024)
+            *reinterpret_cast<f32x4*>(Xs + i) = *reinterpret_cast<const f32x4*>(xg + i);
+        for (int i = cnt4 + tid; i < BM * fin; i += 256) Xs[i] = i < cnt ? xg[i] : 0.f;
+    }
+    // W [HF, fin] contiguous (16-B aligned: a fresh torch allocation); rows >= HF are zero
+    {
+        const int cnt = HF * fin, cnt4 = cnt & ~3;
+        for (int i = tid * 4; i < cnt4; i += 1024)
+            *reinterpret_cast<f32x4*>(Ws + i) = *reinterpret_cast<const f32x4*>(W + i);
+        for (int i = cnt4 + tid; i < BN * fin; i += 256) Ws[i] = i < cnt ? W[i] : 0.f;
+    }
+    __syncthreads();
+
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* xa = Xs + (w * 16 + cl) * fin + kq;
+    const float* wb = Ws + cl * fin + kq;
+    const int ks = fin / 4;
+    for (int s = 0; s < ks; ++s) {  // full k-steps
+        const float a = xa[4 * s];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[t * 16 * fin + 4 * s], acc[t], 0, 0, 0);
+    }
+    if (fin & 3) {  // last partial k-step
+        const bool ok = 4 * ks + kq < fin;
+        const float a = ok ? xa[4 * ks] : 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const float b = ok ? wb[t * 16 * fin + 4 * ks] : 0.f;
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // X/W tiles dead: reuse LDS for the output tile
+
+    float* Os = smem;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int cc = t * 16 + cl;
+        const float bb = cc < HF ? bW[cc] : 0.f;  // Linear bias inside Wh (GAT.py:43)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Os[(w * 16 + kq * 4 + i) * OS + cc] = acc[t][i] + bb;
+    }
+    __syncthreads();
+    const int hfp = round_up4(HF), c4n = hfp / 4;
+    for (int idx = tid; idx < rows * c4n; idx += 256) {
+        const int r = idx / c4n, c4 = idx - r * c4n;
+        f32x4 v = *reinterpret_cast<const f32x4*>(Os + r * OS + 4 * c4);
+        if (4 * c4 + 3 >= HF) {  // zero the pad columns [HF, hfp)
+            if (4 * c4 + 0 >= HF) v.x = 0.f;
+            if (4 * c4 + 1 >= HF) v.y = 0.f;
+            if (4 * c4 + 2 >= HF) v.z = 0.f;
+            if (4 * c4 + 3 >= HF) v.w = 0.f;
+        }
+        *reinterpret_cast<f32x4*>(Wh + (size_t)(row0 + r) * ld_wh + 4 * c4) = v;
+    }
+    // attention Linears on the fp32 Wh (GAT.py:44-45): s = Wh_h . a_h + c_h
+    for (int idx = tid; idx < rows * H; idx += 256) {
+        const int r = idx / H, h = idx - r * H;
+        const float* o = Os + r * OS + h * F;
+        float v1 = 0.f, v2 = 0.f;
+        for (int f = 0; f < F; ++f) {
+            v1 = fmaf(o[f], a1[h * F + f], v1);
+            v2 = fmaf(o[f], a2[h * F + f], v2);
+        }
+        Ss[(size_t)(row0 + r) * ld_s + h] = v1 + c1[h];
+        s_dst[(size_t)(row0 + r) * H + h] = v2 + c2[h];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Edge kernel: one wavefront (= one 64-thread workgroup) per target row.
 //
 // For each chunk of C in-edges of row r:
@@ -775,11 +878,35 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
     const int nt = (hf + 15) / 16;
-    // GAT_PROJ_KERNEL (A/B knob): "direct" (default where F is a power of two),
-    // "tiled" (LDS-tiled, shuffle epilogue), "lds" (LDS-tiled, LDS epilogue)
+    // GAT_PROJ_KERNEL (A/B knob): "wk" (default for fin <= 128: whole K in LDS),
+    // "tiled" (K-tiled, shuffle epilogue; default for larger fin), "lds"
+    // (K-tiled, LDS epilogue), "direct" (register-direct, F a power of two)
     const char* pk = std::getenv("GAT_PROJ_KERNEL");
     const bool pow2_f = next_pow2(f) == f;
-    if (pow2_f && (pk == nullptr || std::strcmp(pk, "direct") == 0)) {
+    const size_t wk_lds = (size_t)(round_up4(64 * fin) + nt * 16 * fin) * sizeof(float);
+    const size_t wk_out = (size_t)64 * (nt * 16 + 4) * sizeof(float);
+    const bool aligned16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) |
+                             reinterpret_cast<uintptr_t>(wh)) & 15) == 0;
+    const bool wk_ok = fin > 0 && fin <= 128 && aligned16 &&
+                       (pk == nullptr || std::strcmp(pk, "wk") == 0);
+    if (wk_ok) {
+        const size_t lds = wk_lds > wk_out ? wk_lds : wk_out;
+#define GAT_WK_CASE(NT)                                                                       \
+    case NT:                                                                                  \
+        hipLaunchKernelGGL((k_project_wk<NT>), grid, block, lds, st, x, n, fin, w, b, a_src,  \
+                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst); \
+        break;
+        switch (nt) {
+            GAT_WK_CASE(1) GAT_WK_CASE(2) GAT_WK_CASE(3) GAT_WK_CASE(4)
+            GAT_WK_CASE(5) GAT_WK_CASE(6) GAT_WK_CASE(7) GAT_WK_CASE(8)
+            GAT_WK_CASE(9) GAT_WK_CASE(10) GAT_WK_CASE(11) GAT_WK_CASE(12)
+            GAT_WK_CASE(13) GAT_WK_CASE(14) GAT_WK_CASE(15) GAT_WK_CASE(16)
+            default: return GAT_EUNSUPPORTED;
+        }
+#undef GAT_WK_CASE
+        return status_of(hipGetLastError());
+    }
+    if (pow2_f && pk != nullptr && std::strcmp(pk, "direct") == 0) {
         int tw = nt < 2 ? nt : 2;
         if (f / 16 > tw) tw = f / 16;
         const int cgroups = (nt + tw - 1) / tw;

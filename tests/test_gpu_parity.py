@@ -31,6 +31,7 @@ VARIANTS = {
     "fast_u16": {"GAT_EDGE_U": "16"},
     "gather_score": {"GAT_EDGE_SCORE": "gather"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
+    "proj_direct": {"GAT_PROJ_KERNEL": "direct"},
 }
 
 

