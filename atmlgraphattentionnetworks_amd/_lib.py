@@ -31,11 +31,11 @@ SIGNATURES = {
     "gat_table_layout": (_c_int, [_c_int, _c_int, _c_int_p, _c_int_p]),
     "gat_project": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                              _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp]),
-    "gat_edge_aggregate": (_c_int, [_c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_int,
-                                    _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_float,
-                                    _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gat_edge_aggregate": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp,
+                                    _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
+                                    _c_float, _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_csr_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
-    "gat_csr_build": (_c_int, [_c_vp, _c_ll, _c_int, _c_vp, _c_vp, _c_vp, ctypes.c_size_t,
+    "gat_csr_build": (_c_int, [_c_vp, _c_ll, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, ctypes.c_size_t,
                                _c_vp, _c_vp]),
 }
 

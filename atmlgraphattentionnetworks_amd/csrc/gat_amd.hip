@@ -500,7 +500,8 @@ __global__ __launch_bounds__(256) void k_project_wk(
 // ---------------------------------------------------------------------------
 template <int LPE, int HP>
 __global__ __launch_bounds__(64) void k_edge_fwd(
-    const int* __restrict__ rowptr, const int* __restrict__ col, int row_begin, int row_end,
+    const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
+    int row_begin, int row_end,
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
     const float* __restrict__ s_dst,
     int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
@@ -515,8 +516,9 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
     __shared__ float y_s[LPE * 4];
 
     const int lane = threadIdx.x;
-    const int r = row_begin + blockIdx.x;
-    if (r >= row_end) return;
+    const int pos = row_begin + blockIdx.x;
+    if (pos >= row_end) return;
+    const int r = order != nullptr ? order[pos] : pos;
     const int e0 = rowptr[r], e1 = rowptr[r + 1];
 
     const int hs = lane & (HP - 1);
@@ -633,28 +635,31 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 }
 
 // ---------------------------------------------------------------------------
-// Edge kernel, lane-group variant (F % 4 == 0): G = next_pow2(HF/4) lanes per
-// target row, 64/G rows per wave, one row per group.
+// Edge kernel, lane-group variant (F % 4V == 0): G = next_pow2(HF/4)/V lanes
+// per target row, each lane owning V float4s (4V columns of ONE head), 64/G
+// rows per wave, one row per group.
 //
-// Lane c of a group owns the float4 columns [4c, 4c+4) of the row — all in
-// head h = 4c / F — and runs that head's online softmax in registers, so the
-// hot loop has no LDS traffic, no barriers and no cross-lane reductions
-// beyond the score's.  Per chunk of U in-edges: one coalesced col load, U
-// broadcasts by shuffle, then U independent Wh float4 gathers in flight per
-// lane and one rescale per chunk.
+// Each lane runs its head's online softmax in registers, so the hot loop has
+// no LDS traffic, no barriers and no cross-lane reductions beyond the score's.
+// Per chunk of U in-edges: one coalesced col load (software-pipelined: the
+// next chunk's indices are in flight while this chunk gathers), U broadcasts
+// by shuffle, then U*V independent Wh float4 gathers in flight per lane and
+// one rescale per chunk.
 // FUSED: the source score s_src[j,h] = Wh[j,h].a1_h + c1_h is recomputed from
-// the gathered row (4 FMAs + an xor-add over the head's F/4 lanes) instead
+// the gathered row (4V FMAs + a DPP sum over the head's F/4V lanes) instead
 // of being gathered — one VMEM instruction and up to a cache line less per
 // edge.  Softmax runs in log2 units: e' = LeakyReLU(z) * log2(e), p = 2^(e'-m').
-// Head mean (concat=False, F/4 a power of two) is an xor-butterfly over the
-// group.
+// row_order (optional): target rows in descending in-degree order, so the
+// rows sharing a wave have near-equal lengths and the heaviest start first.
+// Head mean (concat=False, F/4V a power of two) is an xor-butterfly.
 // ---------------------------------------------------------------------------
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
-template <int G, int U, bool FUSED>
+template <int G, int U, int V, bool FUSED>
 __global__ __launch_bounds__(256) void k_edge_grp(
-    const int* __restrict__ rowptr, const int* __restrict__ col, int row_begin, int row_end,
+    const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
+    int row_begin, int row_end,
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
     const float* __restrict__ a_src, const float* __restrict__ c_src,
     const float* __restrict__ s_dst, int H, int F, int HF, int concat, float slope,
@@ -664,21 +669,29 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
-    const int r = row_begin + (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
-    if (r >= row_end) return;
-    const bool c_ok = 4 * c < HF;
-    const int coff = c_ok ? 4 * c : 0;
+    const int pos = row_begin + (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    if (pos >= row_end) return;
+    const int r = order != nullptr ? order[pos] : pos;
+    const bool c_ok = 4 * V * c < HF;
+    const int coff = c_ok ? 4 * V * c : 0;
     const int h = coff / F;
-    f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 a4[V];
     float c1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < V; ++q) a4[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (FUSED) {
-        if (c_ok) a4 = *reinterpret_cast<const f32x4*>(a_src + coff);
+        if (c_ok) {
+#pragma unroll
+            for (int q = 0; q < V; ++q) a4[q] = *reinterpret_cast<const f32x4*>(a_src + coff + 4 * q);
+        }
         c1 = c_src[h];
     }
     const int e0 = rowptr[r], e1 = rowptr[r + 1];
     const float sd = s_dst[(size_t)r * H + h];
     float m = -INFINITY, l = 0.f;  // running max in log2 units
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // col indices are software-pipelined: chunk k+U's are in flight while
     // chunk k gathers (loads unconditional, clamped to the row's last edge)
@@ -693,24 +706,35 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         int j[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) j[u] = __shfl(cv[u / G], gbase + (u % G));
-        f32x4 v[U];
+        f32x4 v[U][V];
         float s[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            v[u] = *reinterpret_cast<const f32x4*>(Wh + (size_t)j[u] * ld_wh + coff);
+            const float* row = Wh + (size_t)j[u] * ld_wh + coff;
+#pragma unroll
+            for (int q = 0; q < V; ++q) v[u][q] = *reinterpret_cast<const f32x4*>(row + 4 * q);
             if constexpr (!FUSED) s[u] = Ss[(size_t)j[u] * ld_s + h];
         }
         if constexpr (FUSED) {
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                s[u] = fmaf(v[u].w, a4.w, fmaf(v[u].z, a4.z, fmaf(v[u].y, a4.y, v[u].x * a4.x)));
-            if (F <= 64) {  // the head's F/4 lanes sit in one 16-lane DPP row
+            for (int u = 0; u < U; ++u) {
+                float d = 0.f;
 #pragma unroll
-                for (int u = 0; u < U; ++u) s[u] = group_sum16(s[u], F / 4);
-            } else {
-                for (int off = 1; off < F / 4; off <<= 1)
+                for (int q = 0; q < V; ++q)
+                    d = fmaf(v[u][q].w, a4[q].w, fmaf(v[u][q].z, a4[q].z,
+                        fmaf(v[u][q].y, a4[q].y, fmaf(v[u][q].x, a4[q].x, d))));
+                s[u] = d;
+            }
+            const int hl = F / (4 * V);  // lanes per head
+            if (hl > 1) {
+                if (hl <= 16) {  // the head's lanes sit in one 16-lane DPP row
 #pragma unroll
-                    for (int u = 0; u < U; ++u) s[u] += __shfl_xor(s[u], off);
+                    for (int u = 0; u < U; ++u) s[u] = group_sum16(s[u], hl);
+                } else {
+                    for (int off = 1; off < hl; off <<= 1)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) s[u] += __shfl_xor(s[u], off);
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) s[u] += c1;
@@ -725,12 +749,14 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         const float m_new = fmaxf(m, emax);
         const float scale = __builtin_amdgcn_exp2f(m - m_new);
         l *= scale;
-        acc *= scale;
+#pragma unroll
+        for (int q = 0; q < V; ++q) acc[q] *= scale;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
             l += p;
-            acc += p * v[u];
+#pragma unroll
+            for (int q = 0; q < V; ++q) acc[q] += p * v[u][q];
         }
         m = m_new;
 #pragma unroll
@@ -738,31 +764,42 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     }
 
     const float inv = 1.f / (l + 1e-16f);
-    f32x4 y = acc * inv;
     if (lse != nullptr && c_ok && (coff % F) == 0)
         lse[(size_t)r * H + h] = (m + log2f(l)) * kLn2;  // natural-log units
     if (concat) {
         if (c_ok) {
-            const f32x4 b = *reinterpret_cast<const f32x4*>(bias + coff);
-            *reinterpret_cast<f32x4*>(out + (size_t)r * ld_out + coff) = y + b;
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                const f32x4 b = *reinterpret_cast<const f32x4*>(bias + coff + 4 * q);
+                *reinterpret_cast<f32x4*>(out + (size_t)r * ld_out + coff + 4 * q) = acc[q] * inv + b;
+            }
         }
     } else {
-        if (!c_ok) y = f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 y[V];
+#pragma unroll
+        for (int q = 0; q < V; ++q) y[q] = c_ok ? acc[q] * inv : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int off = G / 2; off >= 1; off >>= 1) {
-            if (off < F / 4) break;
-            y.x += __shfl_xor(y.x, off);
-            y.y += __shfl_xor(y.y, off);
-            y.z += __shfl_xor(y.z, off);
-            y.w += __shfl_xor(y.w, off);
+            if (off < F / (4 * V)) break;
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                y[q].x += __shfl_xor(y[q].x, off);
+                y[q].y += __shfl_xor(y[q].y, off);
+                y[q].z += __shfl_xor(y[q].z, off);
+                y[q].w += __shfl_xor(y[q].w, off);
+            }
         }
-        if (4 * c < F) {
+        if (4 * V * c < F) {
             const float hh = (float)H;
-            float* o = out + (size_t)r * ld_out + 4 * c;
-            o[0] = y.x / hh + bias[4 * c + 0];
-            o[1] = y.y / hh + bias[4 * c + 1];
-            o[2] = y.z / hh + bias[4 * c + 2];
-            o[3] = y.w / hh + bias[4 * c + 3];
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                const int f0 = 4 * V * c + 4 * q;
+                float* o = out + (size_t)r * ld_out + f0;
+                o[0] = y[q].x / hh + bias[f0 + 0];
+                o[1] = y[q].y / hh + bias[f0 + 1];
+                o[2] = y[q].z / hh + bias[f0 + 2];
+                o[3] = y[q].w / hh + bias[f0 + 3];
+            }
         }
     }
 }
@@ -806,6 +843,15 @@ __global__ void k_csr_scatter(const unsigned* __restrict__ sorted_keys,
         col[rowptr[i + 1] - 1] = (int)i;  // the appended self-loop closes each row
 }
 
+__global__ void k_degree_keys(const int* __restrict__ rowptr, int n, unsigned* __restrict__ keys,
+                              int* __restrict__ rows) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+        keys[i] = (unsigned)(rowptr[i + 1] - rowptr[i]);
+        rows[i] = (int)i;
+    }
+}
+
 constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
@@ -820,6 +866,15 @@ size_t radix_tmp_bytes(long long E, int n) {
     unsigned* k = nullptr;
     int* v = nullptr;
     const hipError_t e = rocprim::radix_sort_pairs(nullptr, tmp, k, k, v, v, (size_t)E, 0u, key_bits(n));
+    return e == hipSuccess ? tmp : 0;
+}
+
+size_t degree_sort_tmp_bytes(int n) {
+    size_t tmp = 0;
+    unsigned* k = nullptr;
+    int* v = nullptr;
+    const hipError_t e = rocprim::radix_sort_pairs_desc(nullptr, tmp, k, k, v, v,
+                                                        (size_t)(n > 0 ? n : 1), 0u, 32u);
     return e == hipSuccess ? tmp : 0;
 }
 
@@ -950,11 +1005,11 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     return status_of(hipGetLastError());
 }
 
-int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row_end,
-                       const float* wh, int ld_wh, const float* s_src, int ld_s,
+int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, int row_begin,
+                       int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
                        const float* a_src, const float* c_src, const float* s_dst, int heads,
                        int f, int concat, float negative_slope, const float* bias, float* out,
-                       float* lse, void* stream) {
+                       float* lse, int edges_per_row_hint, void* stream) {
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
@@ -966,41 +1021,59 @@ int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row
     if (rows == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
     const int ld_out = concat ? hf : f;
-    const int g = next_pow2((hf + 3) / 4);
-    const bool pow2_f4 = (f % 4 == 0) && next_pow2(f / 4) == f / 4;
     const bool slope_ok = negative_slope >= 0.f && negative_slope <= 1.f;
-    const bool grp_ok = (f % 4 == 0) && (concat || pow2_f4) && slope_ok;
-    // fused source score: needs the head's lanes to form an aligned power-of-two block
-    bool fused = grp_ok && pow2_f4 && have_a;
+    // V float4s per lane (one head per lane needs f % 4V == 0): fewer, fuller
+    // waves; GAT_EDGE_V overrides
+    int vv = 1;
+    if (const char* ev = std::getenv("GAT_EDGE_V")) vv = std::atoi(ev);
+    if (vv != 1 && vv != 2 && vv != 4) vv = 1;
+    while (vv > 1 && f % (4 * vv) != 0) vv >>= 1;
+    const int hl = f / (4 * vv);  // lanes per head
+    const bool pow2_hl = (f % (4 * vv) == 0) && next_pow2(hl) == hl;
+    const int g = next_pow2((hf + 4 * vv - 1) / (4 * vv));
+    const bool grp_ok = (f % 4 == 0) && (concat || pow2_hl) && slope_ok;
+    // fused source score: the head's lanes must form an aligned power-of-two block
+    bool fused = grp_ok && pow2_hl && have_a;
     if (fused && s_src != nullptr) fused = kernel_choice("GAT_EDGE_SCORE", "fused", "gather");
     if (s_src == nullptr && !fused) return GAT_EUNSUPPORTED;
     if (grp_ok && (s_src == nullptr || kernel_choice("GAT_EDGE_KERNEL", "group", "generic"))) {
-        const int u = edge_unroll();
+        // edges per chunk: short rows want short chunks (less padding), long rows
+        // more loads in flight; GAT_EDGE_U overrides
+        int u = edges_per_row_hint <= 0 ? 8 : edges_per_row_hint <= 12 ? 4
+              : edges_per_row_hint <= 64 ? 8 : 16;
+        if (const char* eu = std::getenv("GAT_EDGE_U")) u = std::atoi(eu);
         const long long threads = (long long)rows * g;
         const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
-#define GAT_GRP_LAUNCH(G, UU)                                                                  \
+#define GAT_GRP_LAUNCH(G, UU, VV)                                                              \
     if (fused)                                                                                 \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, true>), grid, block, 0, st, rowptr, col,         \
-                           row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,    \
-                           heads, f, hf, concat, negative_slope, bias, out, ld_out, lse);      \
+        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, true>), grid, block, 0, st, rowptr, col,     \
+                           row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src,       \
+                           c_src, s_dst, heads, f, hf, concat, negative_slope, bias, out,      \
+                           ld_out, lse);                                                       \
     else                                                                                       \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, false>), grid, block, 0, st, rowptr, col,        \
-                           row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,    \
-                           heads, f, hf, concat, negative_slope, bias, out, ld_out, lse)
-#define GAT_GRP_U(G)                            \
-    if (u == 4) { GAT_GRP_LAUNCH(G, 4); }       \
-    else if (u == 16) { GAT_GRP_LAUNCH(G, 16); } \
-    else { GAT_GRP_LAUNCH(G, 8); }
-        switch (g) {
-            case 1: GAT_GRP_U(1) break;
-            case 2: GAT_GRP_U(2) break;
-            case 4: GAT_GRP_U(4) break;
-            case 8: GAT_GRP_U(8) break;
-            case 16: GAT_GRP_U(16) break;
-            case 32: GAT_GRP_U(32) break;
-            case 64: GAT_GRP_U(64) break;
-            default: return GAT_EUNSUPPORTED;
-        }
+        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, rowptr, col,    \
+                           row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src,       \
+                           c_src, s_dst, heads, f, hf, concat, negative_slope, bias, out,      \
+                           ld_out, lse)
+#define GAT_GRP_U(G, VV)                              \
+    if (u == 4) { GAT_GRP_LAUNCH(G, 4, VV); }         \
+    else if (u == 16) { GAT_GRP_LAUNCH(G, 16, VV); }  \
+    else { GAT_GRP_LAUNCH(G, 8, VV); }
+#define GAT_GRP_G(VV)                                 \
+    switch (g) {                                      \
+        case 1: GAT_GRP_U(1, VV) break;               \
+        case 2: GAT_GRP_U(2, VV) break;               \
+        case 4: GAT_GRP_U(4, VV) break;               \
+        case 8: GAT_GRP_U(8, VV) break;               \
+        case 16: GAT_GRP_U(16, VV) break;             \
+        case 32: GAT_GRP_U(32, VV) break;             \
+        case 64: GAT_GRP_U(64, VV) break;             \
+        default: return GAT_EUNSUPPORTED;             \
+    }
+        if (vv == 4) { GAT_GRP_G(4) }
+        else if (vv == 2) { GAT_GRP_G(2) }
+        else { GAT_GRP_G(1) }
+#undef GAT_GRP_G
 #undef GAT_GRP_U
 #undef GAT_GRP_LAUNCH
         return status_of(hipGetLastError());
@@ -1009,7 +1082,8 @@ int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row
     const int hp = next_pow2(heads);
     const dim3 grid(rows), block(kWave);
 #define GAT_EDGE_LAUNCH(L, P)                                                                \
-    hipLaunchKernelGGL((k_edge_fwd<L, P>), grid, block, 0, st, rowptr, col, row_begin,       \
+    hipLaunchKernelGGL((k_edge_fwd<L, P>), grid, block, 0, st, rowptr, col, row_order,       \
+                       row_begin,                                                            \
                        row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,              \
                        negative_slope, bias, out, ld_out, lse)
 #define GAT_EDGE_HP(L)                                                                       \
@@ -1041,14 +1115,17 @@ int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes) {
     if (num_edges < 0 || num_nodes < 0 || bytes == nullptr) return GAT_EINVAL;
     if (num_edges + num_nodes > 0x7fffffffLL) return GAT_EUNSUPPORTED;
-    const size_t e = (size_t)(num_edges > 0 ? num_edges : 1);
-    *bytes = 4 * align_up(e * 4) + align_up(radix_tmp_bytes(num_edges, num_nodes > 0 ? num_nodes : 1));
+    long long m = num_edges > num_nodes ? num_edges : num_nodes;
+    if (m < 1) m = 1;
+    const size_t t1 = radix_tmp_bytes(num_edges, num_nodes > 0 ? num_nodes : 1);
+    const size_t t2 = degree_sort_tmp_bytes(num_nodes);
+    *bytes = 4 * align_up((size_t)m * 4) + align_up(t1 > t2 ? t1 : t2);
     return GAT_OK;
 }
 
 int gat_csr_build(const long long* edge_index, long long num_edges, int num_nodes, int* rowptr,
-                  int* col, void* workspace, size_t workspace_bytes, int* error_flag,
-                  void* stream) {
+                  int* col, int* row_order, void* workspace, size_t workspace_bytes,
+                  int* error_flag, void* stream) {
     if (num_edges < 0 || num_nodes < 0 || error_flag == nullptr) return GAT_EINVAL;
     size_t need = 0;
     int rc = gat_csr_workspace_size(num_edges, num_nodes, &need);
@@ -1066,7 +1143,8 @@ int gat_csr_build(const long long* edge_index, long long num_edges, int num_node
         return status_of(hipMemsetAsync(rowptr, 0, sizeof(int), st));
     }
     const long long E = num_edges;
-    const size_t eb = align_up((size_t)(E > 0 ? E : 1) * 4);
+    const long long mm = E > num_nodes ? E : num_nodes;
+    const size_t eb = align_up((size_t)(mm > 0 ? mm : 1) * 4);
     char* ws = (char*)workspace;
     unsigned* keys_in = (unsigned*)(ws);
     int* vals_in = (int*)(ws + eb);
@@ -1085,6 +1163,15 @@ int gat_csr_build(const long long* edge_index, long long num_edges, int num_node
                        keys_out, E, num_nodes, rowptr);
     hipLaunchKernelGGL(k_csr_scatter, dim3(grid_for(E > num_nodes ? E : num_nodes, 256)),
                        dim3(256), 0, st, keys_out, vals_out, E, num_nodes, rowptr, col);
+    if (row_order != nullptr) {
+        // rows by descending in-degree (stable): the edge kernel's schedule
+        hipLaunchKernelGGL(k_degree_keys, dim3(grid_for(num_nodes, 256)), dim3(256), 0, st,
+                           rowptr, num_nodes, keys_in, vals_in);
+        size_t tmp_bytes = need - 4 * eb;
+        e = rocprim::radix_sort_pairs_desc(tmp, tmp_bytes, keys_in, keys_out, vals_in, row_order,
+                                           (size_t)num_nodes, 0u, 32u, st);
+        if (e != hipSuccess) return status_of(e);
+    }
     return status_of(hipGetLastError());
 }
 

@@ -54,6 +54,13 @@ class LocalCSR:
     col: torch.Tensor  # int32 table-row ids
     num_nodes: int  # n_local rows
     num_edges: int
+    order: Optional[torch.Tensor] = None  # int32 [n_local], rows by descending in-degree
+
+
+def degree_order(rowptr: torch.Tensor) -> torch.Tensor:
+    """Rows by descending in-degree, stable (the same schedule gat_csr_build emits)."""
+    deg = (rowptr[1:] - rowptr[:-1]).to(torch.int64)
+    return torch.argsort(deg, descending=True, stable=True).to(torch.int32)
 
 
 def remap_to_table(col: torch.Tensor, bounds: List[int], rows_per_part: int) -> torch.Tensor:
@@ -112,8 +119,8 @@ class ShardedGAT:
         else:
             col = col.clone()
             n_table = csr.num_nodes
-        self.local = LocalCSR((rp[self.r0:self.r1 + 1] - e0).to(torch.int32).contiguous(),
-                              col.contiguous(), self.n_local, e1 - e0)
+        lrp = (rp[self.r0:self.r1 + 1] - e0).to(torch.int32).contiguous()
+        self.local = LocalCSR(lrp, col.contiguous(), self.n_local, e1 - e0, degree_order(lrp))
         # allgather: one packed buffer [Wh | s_src] per node row, so a single
         # collective moves both (zero-filled: padding rows are defined);
         # replicate: the default separate layout (no collective to feed)

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import collections
 import weakref
-from typing import NamedTuple
+from typing import NamedTuple, Optional
 
 import torch
 
@@ -24,6 +24,7 @@ class CSRGraph(NamedTuple):
     col: torch.Tensor  # int32 [E+N], source node ids, self-loop last per row
     num_nodes: int
     num_edges: int  # E + N (edges after add_self_loops)
+    order: Optional[torch.Tensor] = None  # int32 [N], rows by descending in-degree
 
 
 def _check_edge_index(edge_index: torch.Tensor, device: torch.device) -> torch.Tensor:
@@ -50,16 +51,17 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
         raise ValueError("E + N must fit int32 CSR indices")
     rowptr = torch.empty(num_nodes + 1, dtype=torch.int32, device=dev)
     col = torch.empty(E + num_nodes, dtype=torch.int32, device=dev)
+    order = torch.empty(num_nodes, dtype=torch.int32, device=dev)
     ws = torch.empty(_lib.csr_workspace_size(E, num_nodes), dtype=torch.uint8, device=dev)
     flag = torch.empty(1, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
     _lib.check(lib.gat_csr_build(ei.data_ptr(), E, num_nodes, rowptr.data_ptr(), col.data_ptr(),
-                                 ws.data_ptr(), ws.numel(), flag.data_ptr(), stream),
-               "gat_csr_build")
+                                 order.data_ptr(), ws.data_ptr(), ws.numel(), flag.data_ptr(),
+                                 stream), "gat_csr_build")
     if int(flag.item()) != 0:
         # PyG's index_select raises on the same input (GAT.py:53 -> __lift__)
         raise ValueError(f"edge_index contains node ids outside [0, {num_nodes})")
-    return CSRGraph(rowptr, col, num_nodes, E + num_nodes)
+    return CSRGraph(rowptr, col, num_nodes, E + num_nodes, order)
 
 
 class _CSRCache:

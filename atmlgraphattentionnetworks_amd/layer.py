@@ -16,6 +16,7 @@ No PyG import, no CPU path: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import os
 from typing import NamedTuple, Optional, Tuple
 
 import torch
@@ -124,12 +125,16 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
     width = heads * f if concat else f
     if out is None:
         out = torch.empty(rows, width, dtype=torch.float32, device=table.wh.device)
+    order = getattr(csr, "order", None)
+    if order is not None and os.environ.get("GAT_EDGE_ORDER") == "natural":  # A/B knob
+        order = None
+    hint = csr.num_edges // max(csr.num_nodes, 1)
     _lib.check(lib.gat_edge_aggregate(
-        csr.rowptr.data_ptr(), csr.col.data_ptr(), row_begin, rows, table.wh.data_ptr(),
-        table.ld_wh, table.s_src.data_ptr(), table.ld_s,
+        csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
+        row_begin, rows, table.wh.data_ptr(), table.ld_wh, table.s_src.data_ptr(), table.ld_s,
         0 if pp is None else pp.a_src.data_ptr(), 0 if pp is None else pp.c_src.data_ptr(),
         s_dst.data_ptr(), heads, f, int(concat), float(negative_slope), bias.data_ptr(),
-        out.data_ptr(), 0 if lse is None else lse.data_ptr(), _stream(table.wh.device)),
+        out.data_ptr(), 0 if lse is None else lse.data_ptr(), hint, _stream(table.wh.device)),
         "gat_edge_aggregate")
     return out
 

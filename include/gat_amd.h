@@ -78,10 +78,14 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
 
 /*
  * Fused per-edge score + LeakyReLU + segmented softmax + attention-weighted
- * aggregation + concat/head-mean + bias over target rows [row_begin, row_end).
+ * aggregation + concat/head-mean + bias.
  * Replaces GAT.py:53-67 (PyG propagate/__collect__, message, utils.softmax,
  * aggregate aggr='add') and GAT.py:54 (+ bias).
  *   rowptr/col   CSR by target (gat_csr_build); col holds source row ids into wh/s_src
+ *   row_order    optional [rows] permutation of target rows (gat_csr_build's
+ *                degree order); the kernel processes rows row_order[row_begin ..
+ *                row_end) — or rows row_begin .. row_end when NULL.  Only the
+ *                schedule changes; every row's result is the same.
  *   wh           as written by gat_project (or an all-gathered copy)
  *   s_src, ld_s  the source term per node, as written by gat_project; may be NULL
  *                when a_src/c_src are given
@@ -94,14 +98,16 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
  *   out          [rows, heads*f] if concat else [rows, f], indexed by target row
  *   lse          optional [rows, heads] = max + log(sum exp) per (row, head)
  *                (natural log; for the backward pass); may be NULL
+ *   edges_per_row_hint  average in-degree (E'/rows) or 0 if unknown: picks the
+ *                edge-chunk length, never affects results
  * GAT_EUNSUPPORTED if s_src is NULL and the shape needs it (f % 4 != 0, or
  * f/4 not a power of two, or negative_slope outside [0, 1]).
  */
-int gat_edge_aggregate(const int* rowptr, const int* col, int row_begin, int row_end,
-                       const float* wh, int ld_wh, const float* s_src, int ld_s,
+int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, int row_begin,
+                       int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
                        const float* a_src, const float* c_src, const float* s_dst, int heads,
                        int f, int concat, float negative_slope, const float* bias, float* out,
-                       float* lse, void* stream);
+                       float* lse, int edges_per_row_hint, void* stream);
 
 /* Workspace bytes gat_csr_build needs for (num_edges, num_nodes). */
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);
@@ -112,13 +118,15 @@ int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);
  * edges by edge_index[1] that PyG's propagate/softmax/scatter perform (GAT.py:53,60).
  *   edge_index [2, num_edges] int64 (row 0 = source, row 1 = target)
  *   rowptr     [num_nodes + 1] int32,  col [num_edges + num_nodes] int32
+ *   row_order  optional [num_nodes] int32: rows by descending in-degree (stable),
+ *              the schedule gat_edge_aggregate takes; may be NULL
  * Within a row the input edge order is kept and the loop comes last, matching
  * cat([edge_index, loops]).  Existing self-loops and multi-edges are kept.
  * *error_flag (device int) is set non-zero if any index is outside [0, num_nodes).
  */
 int gat_csr_build(const long long* edge_index, long long num_edges, int num_nodes, int* rowptr,
-                  int* col, void* workspace, size_t workspace_bytes, int* error_flag,
-                  void* stream);
+                  int* col, int* row_order, void* workspace, size_t workspace_bytes,
+                  int* error_flag, void* stream);
 
 #ifdef __cplusplus
 }

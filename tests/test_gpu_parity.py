@@ -32,12 +32,15 @@ VARIANTS = {
     "gather_score": {"GAT_EDGE_SCORE": "gather"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
     "proj_direct": {"GAT_PROJ_KERNEL": "direct"},
+    "v2": {"GAT_EDGE_V": "2"},
+    "v4_natural": {"GAT_EDGE_V": "4", "GAT_EDGE_ORDER": "natural"},
 }
 
 
 @pytest.fixture(params=list(VARIANTS))
 def variant(request, monkeypatch):
-    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE"):
+    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
+              "GAT_EDGE_ORDER"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -140,6 +143,10 @@ def test_csr_bit_exact():
     assert np.array_equal(csr.rowptr.cpu().numpy(), exp_rowptr)
     assert np.array_equal(csr.col.cpu().numpy(), exp_col)
     assert csr.num_edges == e + n
+    # schedule: rows by descending in-degree, ties in row order
+    deg = np.diff(exp_rowptr)
+    exp_order = np.lexsort((np.arange(n), -deg)).astype(np.int32)
+    assert np.array_equal(csr.order.cpu().numpy(), exp_order)
 
 
 def test_out_of_range_edge_raises():

@@ -54,16 +54,13 @@ def test_argument_validation_without_gpu():
                            None, 65, None, None) == _lib.GAT_EUNSUPPORTED
     assert lib.gat_project(None, 10, 4, None, None, None, None, None, None, 2, 3, None, 6,
                            None, 2, None, None) == _lib.GAT_EINVAL  # ld_wh not 16-B aligned
-    E = lib.gat_edge_aggregate
-    assert E(None, None, 0, 10, None, 2, 1, 2, None, None, None, 2, 2, 1, 0.2, None, None, None,
-             None) == _lib.GAT_EINVAL  # ld_wh < H*F
-    assert E(None, None, 0, 10, None, 4, 1, 1, None, None, None, 2, 2, 1, 0.2, None, None, None,
-             None) == _lib.GAT_EINVAL  # ld_s < H
-    assert E(None, None, 0, 10, None, 4, None, 2, None, None, None, 2, 2, 1, 0.2, None, None,
-             None, None) == _lib.GAT_EINVAL  # neither s_src nor (a_src, c_src)
-    # zero rows: nothing to launch
-    assert E(None, None, 5, 5, None, 4, 1, 2, None, None, None, 2, 2, 1, 0.2, None, None, None,
-             None) == _lib.GAT_OK
+    def E(rb, re_, ld_wh, s_src, ld_s):
+        return lib.gat_edge_aggregate(None, None, None, rb, re_, None, ld_wh, s_src, ld_s, None,
+                                      None, None, 2, 2, 1, 0.2, None, None, None, 0, None)
+    assert E(0, 10, 2, 1, 2) == _lib.GAT_EINVAL  # ld_wh < H*F
+    assert E(0, 10, 4, 1, 1) == _lib.GAT_EINVAL  # ld_s < H
+    assert E(0, 10, 4, None, 2) == _lib.GAT_EINVAL  # neither s_src nor (a_src, c_src)
+    assert E(5, 5, 4, 1, 2) == _lib.GAT_OK  # zero rows: nothing to launch
     with pytest.raises(_lib.GatLibraryError):
         _lib.check(_lib.GAT_EUNSUPPORTED, "x")
 

@@ -17,10 +17,16 @@ import torch  # noqa: E402
 
 EDGE_VARIANTS = {
     "generic": {"GAT_EDGE_KERNEL": "generic"},
-    "grp_gather_u8": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_U": "8"},
-    "grp_fused_u4": {"GAT_EDGE_U": "4"},
-    "grp_fused_u8": {"GAT_EDGE_U": "8"},
-    "grp_fused_u16": {"GAT_EDGE_U": "16"},
+    "gather_v1": {"GAT_EDGE_SCORE": "gather"},
+    "fused_v1": {},
+    "fused_v1_natural": {"GAT_EDGE_ORDER": "natural"},
+    "fused_v2": {"GAT_EDGE_V": "2"},
+    "fused_v2_natural": {"GAT_EDGE_V": "2", "GAT_EDGE_ORDER": "natural"},
+    "fused_v2_u4": {"GAT_EDGE_V": "2", "GAT_EDGE_U": "4"},
+    "fused_v2_u8": {"GAT_EDGE_V": "2", "GAT_EDGE_U": "8"},
+    "fused_v2_u16": {"GAT_EDGE_V": "2", "GAT_EDGE_U": "16"},
+    "fused_v1_u4": {"GAT_EDGE_U": "4"},
+    "fused_v1_u16": {"GAT_EDGE_U": "16"},
 }
 REF_MM = True  # also time torch.mm(x, W^T) (hipBLASLt) as a projection reference point
 PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "tiled": {"GAT_PROJ_KERNEL": "tiled"},
@@ -28,7 +34,8 @@ PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "tiled": {"GAT_PROJ_KERN
 
 
 def set_env(d):
-    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE"):
+    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
+              "GAT_EDGE_ORDER"):
         os.environ.pop(k, None)
     os.environ.update(d)
 
