@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void k_project_direct(
 }
 
 // ---------------------------------------------------------------------------
-// Projection, whole-K variant (fin <= 128): the workgroup's 64 X rows are one
+// Projection, whole-K variant (fin <= 64): the workgroup's 64 X rows are one
 // contiguous 64*fin*4-byte chunk of HBM, and W [HF, fin] is contiguous too, so
 // both are staged into LDS with fully coalesced float4 loads (16x fewer
 // memory requests than per-row fragment loads) and the MFMAs read their A/B
@@ -409,20 +409,34 @@ __global__ __launch_bounds__(256) void k_project_wk(
     float* Xs = smem;
     float* Ws = smem + xs_n;
 
-    // X rows [row0, row0+rows): one contiguous chunk; row0*fin*4 = 256*b*fin bytes is 16-B aligned
+    // X rows [row0, row0+rows) are one contiguous chunk (row0*fin*4 = 256*b*fin bytes:
+    // 16-B aligned) and W [HF, fin] another.  Each thread issues ALL its float4
+    // loads first (fixed count, clamped addresses: a load->ds_write loop with a
+    // runtime trip count waits on every load), then writes LDS.
     {
+        constexpr int XIT = BM * 64 / 1024, WIT = BN * 64 / 1024;  // fin <= 64
         const float* xg = X + (size_t)row0 * fin;
-        const int cnt = rows * fin, cnt4 = cnt & ~3;
-        for (int i = tid * 4; i < cnt4; i += 1024)
-            *reinterpret_cast<f32x4*>(Xs + i) = *reinterpret_cast<const f32x4*>(xg + i);
-        for (int i = cnt4 + tid; i < BM * fin; i += 256) Xs[i] = i < cnt ? xg[i] : 0.f;
-    }
-    // W [HF, fin] contiguous (16-B aligned: a fresh torch allocation); rows >= HF are zero
-    {
-        const int cnt = HF * fin, cnt4 = cnt & ~3;
-        for (int i = tid * 4; i < cnt4; i += 1024)
-            *reinterpret_cast<f32x4*>(Ws + i) = *reinterpret_cast<const f32x4*>(W + i);
-        for (int i = cnt4 + tid; i < BN * fin; i += 256) Ws[i] = i < cnt ? W[i] : 0.f;
+        const int xc = rows * fin, xc4 = xc & ~3;
+        const int wc = HF * fin, wc4 = wc & ~3;
+        f32x4 xv[XIT], wv[WIT];
+#pragma unroll
+        for (int it = 0; it < XIT; ++it)
+            xv[it] = *reinterpret_cast<const f32x4*>(xg + min(tid * 4 + it * 1024, max(xc4 - 4, 0)));
+#pragma unroll
+        for (int it = 0; it < WIT; ++it)
+            wv[it] = *reinterpret_cast<const f32x4*>(W + min(tid * 4 + it * 1024, max(wc4 - 4, 0)));
+#pragma unroll
+        for (int it = 0; it < XIT; ++it) {
+            const int i = tid * 4 + it * 1024;
+            if (i < xc4) *reinterpret_cast<f32x4*>(Xs + i) = xv[it];
+        }
+#pragma unroll
+        for (int it = 0; it < WIT; ++it) {
+            const int i = tid * 4 + it * 1024;
+            if (i < wc4) *reinterpret_cast<f32x4*>(Ws + i) = wv[it];
+        }
+        for (int i = xc4 + tid; i < BM * fin; i += 256) Xs[i] = i < xc ? xg[i] : 0.f;
+        for (int i = wc4 + tid; i < BN * fin; i += 256) Ws[i] = i < wc ? W[i] : 0.f;
     }
     __syncthreads();
 
@@ -432,7 +446,22 @@ __global__ __launch_bounds__(256) void k_project_wk(
     const float* xa = Xs + (w * 16 + cl) * fin + kq;
     const float* wb = Ws + cl * fin + kq;
     const int ks = fin / 4;
-    for (int s = 0; s < ks; ++s) {  // full k-steps
+    int s = 0;
+    for (; s + 4 <= ks; s += 4) {  // 4 full k-steps per iteration: LDS reads batched
+        float a[4], bq[4][NT];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a[u] = xa[4 * (s + u)];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) bq[u][t] = wb[t * 16 * fin + 4 * (s + u)];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bq[u][t], acc[t], 0, 0, 0);
+    }
+    for (; s < ks; ++s) {
         const float a = xa[4 * s];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -942,7 +971,7 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     const size_t wk_out = (size_t)64 * (nt * 16 + 4) * sizeof(float);
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) |
                              reinterpret_cast<uintptr_t>(wh)) & 15) == 0;
-    const bool wk_ok = fin > 0 && fin <= 128 && aligned16 &&
+    const bool wk_ok = fin > 0 && fin <= 64 && aligned16 &&
                        (pk == nullptr || std::strcmp(pk, "wk") == 0);
     if (wk_ok) {
         const size_t lds = wk_lds > wk_out ? wk_lds : wk_out;
