@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (v_mfma_f32_16x16x4_f32)
 METRIC = "edges/sec through 8-head GAT layer forward, PPI shape, at 1/2/4/8 MI355X"
 
 
@@ -89,7 +90,11 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="ppi")
-    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of a HIP graph")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each step as a captured HIP graph (default: eager launches, "
+                         "which measured faster: the host enqueue of a step is shorter than its "
+                         "GPU time, and graph replays add a ~9 us gap each)")
+    ap.add_argument("--no-graph", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--edge-iters", type=int, default=50)
     args = ap.parse_args()
@@ -129,7 +134,7 @@ def main():
             step()
         torch.cuda.synchronize()
         graph = None
-        if not args.no_graph:
+        if args.graph and not args.no_graph:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
@@ -181,6 +186,7 @@ def main():
         proj_ms = ev0.elapsed_time(ev1) / args.edge_iters
 
     alg_bytes = edge_kernel_bytes(n, n_edges, w.heads, w.out_channels, w.concat)
+    proj_tflops = 2.0 * n * w.in_channels * w.heads * w.out_channels / (proj_ms * 1e-3) / 1e12
     achieved = alg_bytes / (edge_ms * 1e-3) / 1e9
     traffic = load_traffic(args.workload)
     result = {
@@ -205,6 +211,9 @@ def main():
                      "kernel": "k_edge_fwd", "kernel_ms": edge_ms,
                      "algorithmic_bytes_per_launch": alg_bytes},
         "breakdown_ms": {"project": proj_ms, "edge": edge_ms, "csr_build_once": csr_ms},
+        "projection": {"bound": "mfma", "achieved": proj_tflops, "peak": MFMA_F32_PEAK_TFLOPS,
+                       "unit": "TFLOP/s", "frac": proj_tflops / MFMA_F32_PEAK_TFLOPS,
+                       "kernel": "k_project (fp32 MFMA 16x16x4)"},
     }
     if not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(layer.state_dict(), x, ei, w.heads, w.concat,
