@@ -276,7 +276,7 @@ def bench_distributed(args, metric: str):
                        "launch": launch},
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": load_traffic(args.workload),
-                         "kernel": "k_edge_fwd (rank 0 rows)", "kernel_ms": edge_ms,
+                         "kernel": "gat_edge_aggregate (rank 0 rows)", "kernel_ms": edge_ms,
                          "algorithmic_bytes_per_launch": alg},
         }
         print(json.dumps(res), flush=True)

@@ -208,7 +208,7 @@ def main():
                    "parallelism": "single GPU", "launch": "hipGraph" if graph else "eager"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_edge_fwd", "kernel_ms": edge_ms,
+                     "kernel": "gat_edge_aggregate (k_edge_grp)", "kernel_ms": edge_ms,
                      "algorithmic_bytes_per_launch": alg_bytes},
         "breakdown_ms": {"project": proj_ms, "edge": edge_ms, "csr_build_once": csr_ms},
         "projection": {"bound": "mfma", "achieved": proj_tflops, "peak": MFMA_F32_PEAK_TFLOPS,
