@@ -97,12 +97,16 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--edge-iters", type=int, default=50)
+    ap.add_argument("--dist", action="store_true",
+                    help="take the torch.distributed path even at WORLD_SIZE=1 (testing)")
+    ap.add_argument("--no-strong-probe", action="store_true",
+                    help="multi-GPU: skip the strong-scaling all-gather/replicate measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if world > 1 or args.gpus > 1:
+    if world > 1 or args.gpus > 1 or args.dist:
         from atmlgraphattentionnetworks_amd.distributed import bench_distributed
         return bench_distributed(args, METRIC)
 
