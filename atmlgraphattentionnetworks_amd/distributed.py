@@ -271,6 +271,9 @@ def bench_distributed(args, metric: str):
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    # rank 0 prints exactly one JSON line on stdout: keep RCCL's version banner off it
+    if os.environ.get("NCCL_DEBUG", "").upper() in ("", "VERSION"):
+        os.environ["NCCL_DEBUG"] = "WARN"
     dist.init_process_group("nccl", device_id=dev)
 
     w = WORKLOADS[args.workload]
@@ -283,7 +286,19 @@ def bench_distributed(args, metric: str):
     with torch.no_grad():
         for _ in range(3):
             layer(x, ei)
-        t = _time_steps(lambda: layer(x, ei), args.warmup, args.steps, dev)
+        torch.cuda.synchronize()
+        step, launch = (lambda: layer(x, ei)), "eager"
+        if args.graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                layer(x, ei)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                layer(x, ei)
+            step, launch = g.replay, "hipGraph"
+        t = _time_steps(step, args.warmup, args.steps, dev)
         ms = t * 1e3 / args.steps
         e_blk = torch.tensor([csr.num_edges], dtype=torch.float64, device=dev)
         dist.all_reduce(e_blk)
@@ -328,7 +343,7 @@ def bench_distributed(args, metric: str):
                                    f"H={w.heads} F={w.out_channels} concat={w.concat}",
                        "parallelism": f"node-range partition x{world} on block boundaries "
                                       "(empty halo: no collective in the step)",
-                       "launch": "eager"},
+                       "launch": launch},
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": load_traffic(args.workload),
                          "kernel": "gat_edge_aggregate (rank 0 block)", "kernel_ms": edge_ms,
