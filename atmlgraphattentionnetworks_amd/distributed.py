@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import time
 from dataclasses import dataclass
 from typing import List, Optional
@@ -271,9 +272,11 @@ def bench_distributed(args, metric: str):
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    # rank 0 prints exactly one JSON line on stdout: keep RCCL's version banner off it
-    if os.environ.get("NCCL_DEBUG", "").upper() in ("", "VERSION"):
-        os.environ["NCCL_DEBUG"] = "WARN"
+    # rank 0 prints exactly one JSON line on stdout; RCCL prints its banner and
+    # warnings to stdout from C, so fd 1 points at stderr until the result is ready
+    sys.stdout.flush()
+    saved_stdout = os.dup(1)
+    os.dup2(2, 1)
     dist.init_process_group("nccl", device_id=dev)
 
     w = WORKLOADS[args.workload]
@@ -331,6 +334,9 @@ def bench_distributed(args, metric: str):
     from bench import HBM_PEAK_GBS, edge_kernel_bytes, load_traffic  # noqa: E402
     alg = edge_kernel_bytes(n_block, csr.num_edges, w.heads, w.out_channels, w.concat)
     ach = alg / (edge_ms * 1e-3) / 1e9
+    sys.stdout.flush()
+    os.dup2(saved_stdout, 1)
+    os.close(saved_stdout)
     if rank == 0:
         res = {
             "metric": metric, "value": total_edges / (ms * 1e-3), "unit": "edges/s",
