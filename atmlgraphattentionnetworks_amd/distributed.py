@@ -334,9 +334,7 @@ def bench_distributed(args, metric: str):
     from bench import HBM_PEAK_GBS, edge_kernel_bytes, load_traffic  # noqa: E402
     alg = edge_kernel_bytes(n_block, csr.num_edges, w.heads, w.out_channels, w.concat)
     ach = alg / (edge_ms * 1e-3) / 1e9
-    sys.stdout.flush()
-    os.dup2(saved_stdout, 1)
-    os.close(saved_stdout)
+    res = None
     if rank == 0:
         res = {
             "metric": metric, "value": total_edges / (ms * 1e-3), "unit": "edges/s",
@@ -357,6 +355,10 @@ def bench_distributed(args, metric: str):
             "strong_scaling": {"graph": f"one {w.name}-shape graph shared by {world} ranks",
                                "runs": strong},
         }
-        print(json.dumps(res), flush=True)
     dist.barrier()
     dist.destroy_process_group()
+    sys.stdout.flush()
+    os.dup2(saved_stdout, 1)
+    os.close(saved_stdout)
+    if res is not None:
+        print(json.dumps(res), flush=True)
