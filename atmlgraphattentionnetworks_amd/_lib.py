@@ -17,13 +17,14 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 1
+GAT_ABI_VERSION = 2
 GAT_MAX_HEADS = 64
 GAT_MAX_HF = 256
 
 _c_int, _c_ll, _c_float, _c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
 _c_int_p = ctypes.POINTER(ctypes.c_int)
+_c_u64 = ctypes.c_ulonglong
 
 # symbol -> (restype, argtypes); mirrors include/gat_amd.h line for line
 SIGNATURES = {
@@ -37,6 +38,20 @@ SIGNATURES = {
     "gat_csr_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csr_build": (_c_int, [_c_vp, _c_ll, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, ctypes.c_size_t,
                                _c_vp, _c_vp]),
+    "gat_edge_aggregate_train": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
+                                          _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
+                                          _c_int, _c_float, _c_float, _c_u64, _c_vp, _c_vp,
+                                          _c_vp, _c_vp, _c_int, _c_vp]),
+    "gat_csc_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
+    "gat_csc_build": (_c_int, [_c_vp, _c_vp, _c_int, _c_ll, _c_vp, _c_vp, _c_vp, _c_vp,
+                               ctypes.c_size_t, _c_vp]),
+    "gat_edge_backward_rows": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp,
+                                        _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
+                                        _c_int, _c_int, _c_int, _c_float, _c_float, _c_u64,
+                                        _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gat_src_backward": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
+                                  _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int,
+                                  _c_vp, _c_vp, _c_int, _c_vp]),
 }
 
 _lock = threading.Lock()
@@ -96,4 +111,11 @@ def csr_workspace_size(num_edges: int, num_nodes: int) -> int:
     out = ctypes.c_size_t()
     check(load().gat_csr_workspace_size(num_edges, num_nodes, ctypes.byref(out)),
           "gat_csr_workspace_size")
+    return out.value
+
+
+def csc_workspace_size(nnz: int, num_nodes: int) -> int:
+    out = ctypes.c_size_t()
+    check(load().gat_csc_workspace_size(nnz, num_nodes, ctypes.byref(out)),
+          "gat_csc_workspace_size")
     return out.value

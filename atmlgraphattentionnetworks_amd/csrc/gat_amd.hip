@@ -51,6 +51,48 @@ __device__ __forceinline__ float leaky(float z, float slope) {
 
 __host__ __device__ constexpr int round_up4(int v) { return (v + 3) & ~3; }
 
+// Attention dropout (GAT.py:61, F.dropout on the softmax coefficients, training
+// only).  The keep decision for (CSR edge position k, head h) is a pure function
+// of (seed, k, h) — a counter-based hash — so the backward pass regenerates the
+// forward's mask without storing it.  keep <=> mix(seed, k*H + h) >= thresh,
+// thresh = round(p * 2^32); kept coefficients are scaled by 1/(1-p).
+// tests/test_dropout_hash.py restates the hash in numpy.
+struct DropArgs {
+    unsigned thresh;   // 0: no dropout
+    float scale;       // 1 / (1 - p)
+    unsigned seed_lo, seed_hi;
+};
+
+__host__ __device__ __forceinline__ unsigned mix32(unsigned x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+// multiplier applied to a coefficient: scale if kept, 0 if dropped
+__device__ __forceinline__ float drop_factor(const DropArgs& d, long long k, int h, int H) {
+    const unsigned long long idx = (unsigned long long)k * (unsigned)H + (unsigned)h;
+    const unsigned a = mix32((unsigned)idx ^ d.seed_lo);
+    const unsigned b = mix32((unsigned)(idx >> 32) + d.seed_hi);
+    return mix32(a ^ b) >= d.thresh ? d.scale : 0.f;
+}
+
+DropArgs make_drop(float p, unsigned long long seed) {
+    DropArgs d;
+    double t = std::floor((double)p * 4294967296.0 + 0.5);
+    if (t < 0.0) t = 0.0;
+    if (t > 4294967295.0) t = 4294967295.0;
+    d.thresh = (unsigned)t;
+    // p >= 1 drops everything (F.dropout returns zeros)
+    d.scale = p <= 0.f ? 1.f : p >= 1.f ? 0.f : 1.f / (1.f - p);
+    d.seed_lo = (unsigned)seed;
+    d.seed_hi = (unsigned)(seed >> 32);
+    return d;
+}
+
 int next_pow2(int v) {
     int p = 1;
     while (p < v) p <<= 1;
@@ -534,7 +576,8 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
     const float* __restrict__ s_dst,
     int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
-    float* __restrict__ out, int ld_out, float* __restrict__ lse) {
+    float* __restrict__ out, int ld_out, float* __restrict__ lse, DropArgs drop,
+    float* __restrict__ y_heads) {
     constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;  // edges per chunk
     constexpr int R = C * HP / kWave;                          // score slots per lane
     constexpr int EPI = kWave / LPE;                           // edges per gather step
@@ -595,8 +638,11 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const float p = (ev[q] == -INFINITY) ? 0.f : expf(ev[q] - m_new);
-            l_run += p;
-            p_s[lane + kWave * q] = p;
+            l_run += p;  // the softmax denominator never sees the dropout
+            float pd = p;
+            if (drop.thresh != 0u && p != 0.f)
+                pd = p * drop_factor(drop, base + (lane + kWave * q) / HP, hs, H);
+            p_s[lane + kWave * q] = pd;
         }
         if (lane < HP) hv_s[lane] = scale;
         m_run = m_new;
@@ -641,6 +687,11 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
     __syncthreads();
     float y[4] = {acc.x * hv_s[hq[0]], acc.y * hv_s[hq[1]], acc.z * hv_s[hq[2]],
                   acc.w * hv_s[hq[3]]};
+    if (y_heads != nullptr && slot == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (cq[q]) y_heads[(size_t)r * HF + 4 * c + q] = y[q];
+    }
     if (concat) {
         if (slot == 0 && c_ok) {
             float* o = out + (size_t)r * ld_out + 4 * c;
@@ -685,7 +736,7 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
-template <int G, int U, int V, bool FUSED>
+template <int G, int U, int V, bool FUSED, bool DROP>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -693,7 +744,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const float* __restrict__ a_src, const float* __restrict__ c_src,
     const float* __restrict__ s_dst, int H, int F, int HF, int concat, float slope,
     const float* __restrict__ bias, float* __restrict__ out, int ld_out,
-    float* __restrict__ lse) {
+    float* __restrict__ lse, DropArgs drop, float* __restrict__ y_heads) {
     constexpr int CL = (U + G - 1) / G;  // col values held per lane per chunk
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
@@ -783,9 +834,11 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
-            l += p;
+            l += p;  // the softmax denominator never sees the dropout
+            float pa = p;
+            if constexpr (DROP) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
-            for (int q = 0; q < V; ++q) acc[q] += p * v[u][q];
+            for (int q = 0; q < V; ++q) acc[q] += pa * v[u][q];
         }
         m = m_new;
 #pragma unroll
@@ -795,6 +848,11 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const float inv = 1.f / (l + 1e-16f);
     if (lse != nullptr && c_ok && (coff % F) == 0)
         lse[(size_t)r * H + h] = (m + log2f(l)) * kLn2;  // natural-log units
+    if (y_heads != nullptr && c_ok) {
+#pragma unroll
+        for (int q = 0; q < V; ++q)
+            *reinterpret_cast<f32x4*>(y_heads + (size_t)r * HF + coff + 4 * q) = acc[q] * inv;
+    }
     if (concat) {
         if (c_ok) {
 #pragma unroll
@@ -878,6 +936,257 @@ __global__ void k_degree_keys(const int* __restrict__ rowptr, int n, unsigned* _
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
         keys[i] = (unsigned)(rowptr[i + 1] - rowptr[i]);
         rows[i] = (int)i;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// CSC (edges grouped by SOURCE) over the CSR's edge positions, for the
+// backward pass: the gradient of a source row gathers over its out-edges.
+//   csc_ptr[j]       first CSC slot of source j
+//   csc_dst[c]       target row of the edge in CSC slot c
+//   csr_to_csc[k]    CSC slot of CSR position k
+// Built by a stable radix sort of (col[k], k): within a source, edges keep
+// CSR order, so every reduction over them is deterministic.
+// ---------------------------------------------------------------------------
+__global__ void k_edge_rows(const int* __restrict__ rowptr, int n, long long nnz,
+                            int* __restrict__ erow, unsigned* __restrict__ keys,
+                            const int* __restrict__ col, int* __restrict__ vals) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < nnz; k += stride) {
+        // the row holding position k: last i with rowptr[i] <= k
+        int lo = 0, hi = n;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (rowptr[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        erow[k] = lo;
+        keys[k] = (unsigned)col[k];
+        vals[k] = (int)k;
+    }
+}
+
+__global__ void k_csc_ptr(const unsigned* __restrict__ sorted_keys, long long nnz, int n,
+                          int* __restrict__ csc_ptr) {
+    const long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+    if (j > n) return;
+    long long lo = 0, hi = nnz;
+    while (lo < hi) {
+        const long long mid = (lo + hi) >> 1;
+        if (sorted_keys[mid] < (unsigned)j) lo = mid + 1; else hi = mid;
+    }
+    csc_ptr[j] = (int)lo;
+}
+
+__global__ void k_csc_fill(const int* __restrict__ sorted_vals, const int* __restrict__ erow,
+                           long long nnz, int* __restrict__ csc_dst,
+                           int* __restrict__ csr_to_csc) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x; c < nnz; c += stride) {
+        const int k = sorted_vals[c];
+        csr_to_csc[k] = (int)c;
+        csc_dst[c] = erow[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Backward, pass 1: one wave per TARGET row i (CSR), lanes over (edge, head)
+// slots as in k_edge_fwd's score phase.  With dy = dL/dy_heads[i] (concat: the
+// row of g; mean: g[i]/H for every head), y = the forward's normalised
+// per-head aggregation and alpha = exp(e - lse):
+//   delta_h   = dy_h . y_h
+//   dA        = drop * (dy_h . Wh[j]_h)            (A = alpha * drop, drop = keep/(1-p) or 0)
+//   de        = alpha * (dA - delta_h)              softmax backward
+//   dz        = de * (z > 0 ? 1 : slope)            LeakyReLU backward
+//   ds_dst[i] = sum_edges dz
+// and stores A and dz per (edge, head) at the edge's CSC slot, so pass 2
+// reads them contiguously.
+// Algorithmic bytes per edge: 4 (col) + 4 (csr_to_csc) + 4H (s_src) + 4HF (Wh
+// row) + 8H (A, dz); per row: 4HF (g) + 4HF (y) + 8H (s_dst, lse) + 4H.
+// ---------------------------------------------------------------------------
+template <int HP>
+__global__ __launch_bounds__(64) void k_edge_bwd_rows(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
+    int row_begin, int row_end, const int* __restrict__ csr_to_csc,
+    const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
+    const float* __restrict__ s_dst, const float* __restrict__ lse,
+    const float* __restrict__ y_heads, const float* __restrict__ g, int H, int F, int HF,
+    int concat, float slope, DropArgs drop, float* __restrict__ ds_dst,
+    float* __restrict__ alpha_out, float* __restrict__ dz_out) {
+    constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;
+    constexpr int R = C * HP / kWave;
+    __shared__ float dy_s[GAT_MAX_HF];
+    __shared__ float delta_s[HP];
+    __shared__ int col_s[C];
+    __shared__ int slot_s[C];
+
+    const int lane = threadIdx.x;
+    const int pos = row_begin + blockIdx.x;
+    if (pos >= row_end) return;
+    const int r = order != nullptr ? order[pos] : pos;
+    const int e0 = rowptr[r], e1 = rowptr[r + 1];
+    const float inv_h = 1.f / (float)H;
+    for (int c = lane; c < HF; c += kWave)
+        dy_s[c] = concat ? g[(size_t)r * HF + c] : g[(size_t)r * F + (c % F)] * inv_h;
+    __syncthreads();
+    if (lane < H) {
+        float d = 0.f;
+        const float* yr = y_heads + (size_t)r * HF + lane * F;
+        for (int f = 0; f < F; ++f) d = fmaf(dy_s[lane * F + f], yr[f], d);
+        delta_s[lane] = d;
+    }
+    __syncthreads();
+    const int hs = lane & (HP - 1);
+    const bool hs_ok = hs < H;
+    const float sd = hs_ok ? s_dst[(size_t)r * H + hs] : 0.f;
+    const float ls = hs_ok ? lse[(size_t)r * H + hs] : 0.f;
+    const float dl = hs_ok ? delta_s[hs] : 0.f;
+    const float* dyh = dy_s + (hs_ok ? hs : 0) * F;
+    float dsd = 0.f;
+    for (int base = e0; base < e1; base += C) {
+        const int nk = min(C, e1 - base);
+        if (lane < nk) {
+            col_s[lane] = col[base + lane];
+            slot_s[lane] = csr_to_csc[base + lane];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const int k = (lane + kWave * q) / HP;
+            if (k < nk && hs_ok) {
+                const int j = col_s[k];
+                const float z = sd + Ss[(size_t)j * ld_s + hs];
+                const float a = expf(leaky(z, slope) - ls);
+                const float* wr = Wh + (size_t)j * ld_wh + hs * F;
+                float da = 0.f;
+                for (int f = 0; f < F; ++f) da = fmaf(dyh[f], wr[f], da);
+                const float dm = drop.thresh != 0u ? drop_factor(drop, base + k, hs, H) : 1.f;
+                const float de = a * (dm * da - dl);
+                const float dz = z > 0.f ? de : de * slope;
+                dsd += dz;
+                const size_t o = (size_t)slot_s[k] * H + hs;
+                alpha_out[o] = a * dm;
+                dz_out[o] = dz;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int off = HP; off < kWave; off <<= 1) dsd += __shfl_xor(dsd, off);
+    if (lane < H) ds_dst[(size_t)r * H + lane] = dsd;
+}
+
+// ---------------------------------------------------------------------------
+// Backward, pass 2: one wave per SOURCE row j (CSC, grid-stride), lanes over
+// the HF columns (CQ per lane).  Over j's out-edges (target i, slot c):
+//   dWh[j]    = sum_c A[c,h] * dy[i]_h            (message backward)
+//   ds_src[j] = sum_c dz[c]
+// then the score terms s_src = Wh.a1 + c1, s_dst = Wh.a2 + c2 fold in:
+//   dWh_total[j] = dWh[j] + ds_src[j,h] a1_h + ds_dst[j,h] a2_h
+// and each wave accumulates its rows' contributions to da1/da2 (ds * Wh) and
+// dc1/dc2 (ds) in registers, written once as per-wave partials
+// part[w] = [da1 (HF) | da2 (HF) | dc1 (H) | dc2 (H)] — summed by the caller;
+// no float atomics, so the result is run-to-run deterministic.
+// Algorithmic bytes per edge: 4 (csc_dst) + 4HF (g row, concat; 4F mean)
+// + 8H (A, dz); per row: 4HF (Wh) + 4HF (dWh) + 8H.
+// ---------------------------------------------------------------------------
+template <int CQ, int HP>
+__global__ __launch_bounds__(64) void k_src_bwd(
+    const int* __restrict__ csc_ptr, const int* __restrict__ csc_dst, int n,
+    const float* __restrict__ Wh, int ld_wh, const float* __restrict__ g,
+    const float* __restrict__ alpha, const float* __restrict__ dz,
+    const float* __restrict__ ds_dst, const float* __restrict__ a1, const float* __restrict__ a2,
+    int H, int F, int HF, int concat, float* __restrict__ dwh, int ld_dwh,
+    float* __restrict__ ds_src, float* __restrict__ part) {
+    __shared__ float dss_s[HP];
+    const int lane = threadIdx.x;
+    const int w = blockIdx.x;
+    const int nw = gridDim.x;
+    const float inv_h = 1.f / (float)H;
+    int cc[CQ], hq[CQ], gq[CQ];
+    bool okq[CQ];
+    float a1v[CQ], a2v[CQ], pa1[CQ], pa2[CQ];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) {
+        const int c = lane + kWave * q;
+        okq[q] = c < HF;
+        cc[q] = okq[q] ? c : 0;
+        hq[q] = cc[q] / F;
+        gq[q] = concat ? cc[q] : cc[q] - hq[q] * F;  // column of g feeding column c
+        a1v[q] = okq[q] ? a1[cc[q]] : 0.f;
+        a2v[q] = okq[q] ? a2[cc[q]] : 0.f;
+        pa1[q] = 0.f;
+        pa2[q] = 0.f;
+    }
+    const int ldg = concat ? HF : F;
+    const float gs = concat ? 1.f : inv_h;
+    const bool h_ok = lane < H;
+    float pc1 = 0.f, pc2 = 0.f;
+    constexpr int UE = 4;
+    for (int j = w; j < n; j += nw) {
+        const int b0 = csc_ptr[j], b1 = csc_ptr[j + 1];
+        float acc[CQ];
+#pragma unroll
+        for (int q = 0; q < CQ; ++q) acc[q] = 0.f;
+        float dss = 0.f;
+        for (int b = b0; b < b1; b += UE) {
+            int iu[UE], su[UE];
+            float gate[UE];
+#pragma unroll
+            for (int u = 0; u < UE; ++u) {
+                su[u] = min(b + u, b1 - 1);
+                gate[u] = (b + u < b1) ? 1.f : 0.f;
+                iu[u] = csc_dst[su[u]];
+            }
+            float gv[UE][CQ], av[UE][CQ], zv[UE];
+#pragma unroll
+            for (int u = 0; u < UE; ++u) {
+#pragma unroll
+                for (int q = 0; q < CQ; ++q) {
+                    gv[u][q] = g[(size_t)iu[u] * ldg + gq[q]];
+                    av[u][q] = alpha[(size_t)su[u] * H + hq[q]];
+                }
+                zv[u] = h_ok ? dz[(size_t)su[u] * H + lane] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < UE; ++u) {
+#pragma unroll
+                for (int q = 0; q < CQ; ++q) acc[q] = fmaf(gate[u] * av[u][q], gv[u][q], acc[q]);
+                dss = fmaf(gate[u], zv[u], dss);
+            }
+        }
+        if (h_ok) {
+            dss_s[lane] = dss;
+            if (ds_src != nullptr) ds_src[(size_t)j * H + lane] = dss;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < CQ; ++q) {
+            if (okq[q]) {
+                const float hsrc = dss_s[hq[q]];
+                const float hdst = ds_dst[(size_t)j * H + hq[q]];
+                const float whv = Wh[(size_t)j * ld_wh + cc[q]];
+                dwh[(size_t)j * ld_dwh + cc[q]] = fmaf(hdst, a2v[q], fmaf(hsrc, a1v[q], acc[q] * gs));
+                pa1[q] = fmaf(hsrc, whv, pa1[q]);
+                pa2[q] = fmaf(hdst, whv, pa2[q]);
+            }
+        }
+        if (h_ok) {
+            pc1 += dss;
+            pc2 += ds_dst[(size_t)j * H + lane];
+        }
+        __syncthreads();
+    }
+    float* pw = part + (size_t)w * (2 * HF + 2 * H);
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) {
+        if (okq[q]) {
+            pw[cc[q]] = pa1[q];
+            pw[HF + cc[q]] = pa2[q];
+        }
+    }
+    if (h_ok) {
+        pw[2 * HF + lane] = pc1;
+        pw[2 * HF + H + lane] = pc2;
     }
 }
 
@@ -1034,11 +1343,13 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     return status_of(hipGetLastError());
 }
 
-int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, int row_begin,
-                       int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
-                       const float* a_src, const float* c_src, const float* s_dst, int heads,
-                       int f, int concat, float negative_slope, const float* bias, float* out,
-                       float* lse, int edges_per_row_hint, void* stream) {
+static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row_order,
+                               int row_begin, int row_end, const float* wh, int ld_wh,
+                               const float* s_src, int ld_s, const float* a_src,
+                               const float* c_src, const float* s_dst, int heads, int f,
+                               int concat, float negative_slope, const float* bias, float* out,
+                               float* lse, float* y_heads, DropArgs drop,
+                               int edges_per_row_hint, void* stream) {
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
@@ -1053,9 +1364,11 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
     const bool slope_ok = negative_slope >= 0.f && negative_slope <= 1.f;
     // V float4s per lane (one head per lane needs f % 4V == 0): fewer, fuller
     // waves; GAT_EDGE_V overrides
+    const bool dropping = drop.thresh != 0u;
     int vv = 1;
     if (const char* ev = std::getenv("GAT_EDGE_V")) vv = std::atoi(ev);
     if (vv != 1 && vv != 2 && vv != 4) vv = 1;
+    if (dropping) vv = 1;  // the dropout variant is instantiated for V = 1, U = 8 only
     while (vv > 1 && f % (4 * vv) != 0) vv >>= 1;
     const int hl = f / (4 * vv);  // lanes per head
     const bool pow2_hl = (f % (4 * vv) == 0) && next_pow2(hl) == hl;
@@ -1071,22 +1384,28 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
         int u = edges_per_row_hint <= 0 ? 8 : edges_per_row_hint <= 12 ? 4
               : edges_per_row_hint <= 64 ? 8 : 16;
         if (const char* eu = std::getenv("GAT_EDGE_U")) u = std::atoi(eu);
+        if (dropping) u = 8;
         const long long threads = (long long)rows * g;
         const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
-#define GAT_GRP_LAUNCH(G, UU, VV)                                                              \
-    if (fused)                                                                                 \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, true>), grid, block, 0, st, rowptr, col,     \
-                           row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src,       \
-                           c_src, s_dst, heads, f, hf, concat, negative_slope, bias, out,      \
-                           ld_out, lse);                                                       \
-    else                                                                                       \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, rowptr, col,    \
-                           row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src,       \
-                           c_src, s_dst, heads, f, hf, concat, negative_slope, bias, out,      \
-                           ld_out, lse)
-#define GAT_GRP_U(G, VV)                              \
-    if (u == 4) { GAT_GRP_LAUNCH(G, 4, VV); }         \
-    else if (u == 16) { GAT_GRP_LAUNCH(G, 16, VV); }  \
+#define GAT_GRP_ARGS                                                                          \
+    grid, block, 0, st, rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s,    \
+        a_src, c_src, s_dst, heads, f, hf, concat, negative_slope, bias, out, ld_out, lse,     \
+        drop, y_heads
+#define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
+    if (fused)                                                                        \
+        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, true, false>), GAT_GRP_ARGS);       \
+    else                                                                              \
+        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false, false>), GAT_GRP_ARGS)
+#define GAT_GRP_U(G, VV)                                                              \
+    if (dropping) {                                                                   \
+        if (VV == 1) {                                                                \
+            if (fused)                                                                \
+                hipLaunchKernelGGL((k_edge_grp<G, 8, 1, true, true>), GAT_GRP_ARGS);  \
+            else                                                                      \
+                hipLaunchKernelGGL((k_edge_grp<G, 8, 1, false, true>), GAT_GRP_ARGS); \
+        }                                                                             \
+    } else if (u == 4) { GAT_GRP_LAUNCH(G, 4, VV); }                                  \
+    else if (u == 16) { GAT_GRP_LAUNCH(G, 16, VV); }                                  \
     else { GAT_GRP_LAUNCH(G, 8, VV); }
 #define GAT_GRP_G(VV)                                 \
     switch (g) {                                      \
@@ -1105,6 +1424,7 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
 #undef GAT_GRP_G
 #undef GAT_GRP_U
 #undef GAT_GRP_LAUNCH
+#undef GAT_GRP_ARGS
         return status_of(hipGetLastError());
     }
     const int lpe = next_pow2((round_up4(hf) + 3) / 4);
@@ -1113,8 +1433,8 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
 #define GAT_EDGE_LAUNCH(L, P)                                                                \
     hipLaunchKernelGGL((k_edge_fwd<L, P>), grid, block, 0, st, rowptr, col, row_order,       \
                        row_begin,                                                            \
-                       row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,              \
-                       negative_slope, bias, out, ld_out, lse)
+                       row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,         \
+                       negative_slope, bias, out, ld_out, lse, drop, y_heads)
 #define GAT_EDGE_HP(L)                                                                       \
     switch (hp) {                                                                            \
         case 1: GAT_EDGE_LAUNCH(L, 1); break;                                                \
@@ -1139,6 +1459,32 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
 #undef GAT_EDGE_HP
 #undef GAT_EDGE_LAUNCH
     return status_of(hipGetLastError());
+}
+
+int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, int row_begin,
+                       int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
+                       const float* a_src, const float* c_src, const float* s_dst, int heads,
+                       int f, int concat, float negative_slope, const float* bias, float* out,
+                       float* lse, int edges_per_row_hint, void* stream) {
+    return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src,
+                               ld_s, a_src, c_src, s_dst, heads, f, concat, negative_slope, bias,
+                               out, lse, nullptr, make_drop(0.f, 0ull), edges_per_row_hint,
+                               stream);
+}
+
+int gat_edge_aggregate_train(const int* rowptr, const int* col, const int* row_order,
+                             int row_begin, int row_end, const float* wh, int ld_wh,
+                             const float* s_src, int ld_s, const float* a_src, const float* c_src,
+                             const float* s_dst, int heads, int f, int concat,
+                             float negative_slope, float dropout_p, unsigned long long seed,
+                             const float* bias, float* out, float* lse, float* y_heads,
+                             int edges_per_row_hint, void* stream) {
+    if (lse == nullptr || y_heads == nullptr) return GAT_EINVAL;
+    if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
+    return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src,
+                               ld_s, a_src, c_src, s_dst, heads, f, concat, negative_slope, bias,
+                               out, lse, y_heads, make_drop(dropout_p, seed), edges_per_row_hint,
+                               stream);
 }
 
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes) {
@@ -1201,6 +1547,118 @@ int gat_csr_build(const long long* edge_index, long long num_edges, int num_node
                                            (size_t)num_nodes, 0u, 32u, st);
         if (e != hipSuccess) return status_of(e);
     }
+    return status_of(hipGetLastError());
+}
+
+int gat_csc_workspace_size(long long nnz, int num_nodes, size_t* bytes) {
+    if (nnz < 0 || num_nodes < 0 || bytes == nullptr) return GAT_EINVAL;
+    if (nnz > 0x7fffffffLL) return GAT_EUNSUPPORTED;
+    const size_t eb = align_up((size_t)(nnz > 0 ? nnz : 1) * 4);
+    *bytes = 5 * eb + align_up(radix_tmp_bytes(nnz, num_nodes > 0 ? num_nodes : 1));
+    return GAT_OK;
+}
+
+int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nnz, int* csc_ptr,
+                  int* csc_dst, int* csr_to_csc, void* workspace, size_t workspace_bytes,
+                  void* stream) {
+    if (num_nodes < 0 || nnz < 0) return GAT_EINVAL;
+    size_t need = 0;
+    int rc = gat_csc_workspace_size(nnz, num_nodes, &need);
+    if (rc != GAT_OK) return rc;
+    if (workspace_bytes < need) return GAT_EWORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    if (num_nodes == 0) return GAT_OK;
+    if (nnz == 0) return status_of(hipMemsetAsync(csc_ptr, 0, sizeof(int) * (num_nodes + 1), st));
+    const size_t eb = align_up((size_t)nnz * 4);
+    char* ws = (char*)workspace;
+    int* erow = (int*)ws;
+    unsigned* keys_in = (unsigned*)(ws + eb);
+    int* vals_in = (int*)(ws + 2 * eb);
+    unsigned* keys_out = (unsigned*)(ws + 3 * eb);
+    int* vals_out = (int*)(ws + 4 * eb);
+    void* tmp = ws + 5 * eb;
+    hipLaunchKernelGGL(k_edge_rows, dim3(grid_for(nnz, 256)), dim3(256), 0, st, rowptr,
+                       num_nodes, nnz, erow, keys_in, col, vals_in);
+    size_t tmp_bytes = need - 5 * eb;
+    hipError_t e = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out,
+                                             (size_t)nnz, 0u, key_bits(num_nodes), st);
+    if (e != hipSuccess) return status_of(e);
+    hipLaunchKernelGGL(k_csc_ptr, dim3((num_nodes + 1 + 255) / 256), dim3(256), 0, st, keys_out,
+                       nnz, num_nodes, csc_ptr);
+    hipLaunchKernelGGL(k_csc_fill, dim3(grid_for(nnz, 256)), dim3(256), 0, st, vals_out, erow,
+                       nnz, csc_dst, csr_to_csc);
+    return status_of(hipGetLastError());
+}
+
+int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_order,
+                           int row_begin, int row_end, const int* csr_to_csc, const float* wh,
+                           int ld_wh, const float* s_src, int ld_s, const float* s_dst,
+                           const float* lse, const float* y_heads, const float* grad_out,
+                           int heads, int f, int concat, float negative_slope, float dropout_p,
+                           unsigned long long seed, float* ds_dst, float* alpha_csc,
+                           float* dz_csc, void* stream) {
+    if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
+    const int hf = heads * f;
+    if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
+    if (ld_wh < hf || ld_s < heads) return GAT_EINVAL;
+    if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
+    const int rows = row_end - row_begin;
+    if (rows == 0) return GAT_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const DropArgs drop = make_drop(dropout_p, seed);
+    const dim3 grid(rows), block(kWave);
+#define GAT_BWD_ROWS(P)                                                                       \
+    case P:                                                                                   \
+        hipLaunchKernelGGL((k_edge_bwd_rows<P>), grid, block, 0, st, rowptr, col, row_order,  \
+                           row_begin, row_end, csr_to_csc, wh, ld_wh, s_src, ld_s, s_dst, lse, \
+                           y_heads, grad_out, heads, f, hf, concat, negative_slope, drop,     \
+                           ds_dst, alpha_csc, dz_csc);                                        \
+        break;
+    switch (next_pow2(heads)) {
+        GAT_BWD_ROWS(1) GAT_BWD_ROWS(2) GAT_BWD_ROWS(4) GAT_BWD_ROWS(8)
+        GAT_BWD_ROWS(16) GAT_BWD_ROWS(32) GAT_BWD_ROWS(64)
+        default: return GAT_EUNSUPPORTED;
+    }
+#undef GAT_BWD_ROWS
+    return status_of(hipGetLastError());
+}
+
+int gat_src_backward(const int* csc_ptr, const int* csc_dst, int num_nodes, const float* wh,
+                     int ld_wh, const float* grad_out, const float* alpha_csc,
+                     const float* dz_csc, const float* ds_dst, const float* a_src,
+                     const float* a_dst, int heads, int f, int concat, float* dwh, int ld_dwh,
+                     float* ds_src, float* partials, int num_parts, void* stream) {
+    if (heads <= 0 || f <= 0 || num_nodes < 0 || num_parts <= 0) return GAT_EINVAL;
+    const int hf = heads * f;
+    if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
+    if (ld_wh < hf || ld_dwh < hf) return GAT_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid(num_parts), block(kWave);
+    const int cq = (hf + kWave - 1) / kWave;
+#define GAT_SRC_LAUNCH(CQ, P)                                                                 \
+    hipLaunchKernelGGL((k_src_bwd<CQ, P>), grid, block, 0, st, csc_ptr, csc_dst, num_nodes,   \
+                       wh, ld_wh, grad_out, alpha_csc, dz_csc, ds_dst, a_src, a_dst, heads, f, \
+                       hf, concat, dwh, ld_dwh, ds_src, partials)
+#define GAT_SRC_HP(CQ)                                               \
+    switch (next_pow2(heads)) {                                      \
+        case 1: GAT_SRC_LAUNCH(CQ, 1); break;                        \
+        case 2: GAT_SRC_LAUNCH(CQ, 2); break;                        \
+        case 4: GAT_SRC_LAUNCH(CQ, 4); break;                        \
+        case 8: GAT_SRC_LAUNCH(CQ, 8); break;                        \
+        case 16: GAT_SRC_LAUNCH(CQ, 16); break;                      \
+        case 32: GAT_SRC_LAUNCH(CQ, 32); break;                      \
+        case 64: GAT_SRC_LAUNCH(CQ, 64); break;                      \
+        default: return GAT_EUNSUPPORTED;                            \
+    }
+    switch (cq) {
+        case 1: GAT_SRC_HP(1) break;
+        case 2: GAT_SRC_HP(2) break;
+        case 3: GAT_SRC_HP(3) break;
+        case 4: GAT_SRC_HP(4) break;
+        default: return GAT_EUNSUPPORTED;
+    }
+#undef GAT_SRC_HP
+#undef GAT_SRC_LAUNCH
     return status_of(hipGetLastError());
 }
 

@@ -93,3 +93,41 @@ csr_cache = _CSRCache()
 
 def get_csr(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
     return csr_cache.get(edge_index, num_nodes)
+
+
+class CSCGraph(NamedTuple):
+    """Transpose of a CSRGraph over its edge positions (``gat_csc_build``):
+    the backward pass reduces each source row's gradient over its out-edges."""
+    ptr: torch.Tensor  # int32 [N+1], first CSC slot per source node
+    dst: torch.Tensor  # int32 [E'], target row per CSC slot
+    csr_to_csc: torch.Tensor  # int32 [E'], CSC slot of each CSR position
+
+
+def build_csc(csr: CSRGraph) -> CSCGraph:
+    lib = _lib.load()
+    dev = csr.rowptr.device
+    n, nnz = csr.num_nodes, csr.num_edges
+    ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    dst = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    c2c = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    ws = torch.empty(_lib.csc_workspace_size(nnz, n), dtype=torch.uint8, device=dev)
+    _lib.check(lib.gat_csc_build(csr.rowptr.data_ptr(), csr.col.data_ptr(), n, nnz,
+                                 ptr.data_ptr(), dst.data_ptr(), c2c.data_ptr(), ws.data_ptr(),
+                                 ws.numel(), torch.cuda.current_stream(dev).cuda_stream),
+               "gat_csc_build")
+    return CSCGraph(ptr, dst, c2c)
+
+
+_csc_cache = {}
+
+
+def get_csc(csr: CSRGraph) -> CSCGraph:
+    """The CSC of ``csr``, built on first use and kept while ``csr.rowptr`` lives."""
+    key = id(csr.rowptr)
+    hit = _csc_cache.get(key)
+    if hit is not None and hit[0]() is csr.rowptr:
+        return hit[1]
+    csc = build_csc(csr)
+    _csc_cache[key] = (weakref.ref(csr.rowptr), csc)
+    weakref.finalize(csr.rowptr, _csc_cache.pop, key, None)
+    return csc

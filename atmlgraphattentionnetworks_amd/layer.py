@@ -12,6 +12,10 @@ forward (``GAT.py:37-67``) runs entirely in the HIP library:
   3. ``gat_edge_aggregate``: scores, LeakyReLU, segmented softmax,
      weighted aggregation, concat / head-mean, bias (``GAT.py:53-67``).
 
+When autograd needs the result, or in training mode with dropout > 0, the
+forward goes through ``training.GATFunction`` instead: the same two kernels
+plus attention dropout (``GAT.py:61``) and a HIP backward pass.
+
 No PyG import, no CPU path: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
@@ -242,15 +246,14 @@ class GraphAttentionLayer(torch.nn.Module):
     def forward(self, x, edge_index):
         x = _check_x(x, self.input_channels)
         csr = get_csr(edge_index, x.size(0))
-        if self.training and self.dropout_val > 0.0:
-            raise NotImplementedError(
-                "attention dropout in training mode is not implemented in the HIP path yet; "
-                "call .eval() or construct with dropout=0.0")
+        p = float(self.dropout_val) if self.training else 0.0
         needs_grad = torch.is_grad_enabled() and (
-            x.requires_grad or any(p.requires_grad for p in self.parameters()))
-        if needs_grad:
-            raise NotImplementedError("the HIP backward pass is not implemented yet; "
-                                      "run the forward under torch.no_grad()")
+            x.requires_grad or any(p_.requires_grad for p_ in self.parameters()))
+        if needs_grad or p > 0.0:
+            # training path (training.py): dropout of GAT.py:61 and the HIP backward
+            from .training import gat_train_forward, new_dropout_seed
+            seed = new_dropout_seed() if p > 0.0 else 0
+            return gat_train_forward(self, x, csr, p, seed)
         return gat_forward(x, csr, self.packed(), self.bias.detach(), self.num_heads,
                            self.output_channels, self.concat, self.negative_slope)
 

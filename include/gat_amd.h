@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 1
+#define GAT_ABI_VERSION 2
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -127,6 +127,84 @@ int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);
 int gat_csr_build(const long long* edge_index, long long num_edges, int num_nodes, int* rowptr,
                   int* col, int* row_order, void* workspace, size_t workspace_bytes,
                   int* error_flag, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Training: forward with attention dropout, and the backward pass.
+ * Together these replace autograd through GAT.py:37-67 (the reference trains
+ * the layer with loss.backward(), run_inductive.py / run_*_experiment.py).
+ * ------------------------------------------------------------------------- */
+
+/*
+ * gat_edge_aggregate plus what the backward needs.  Replaces GAT.py:53-67 in
+ * training mode, including GAT.py:61 (F.dropout on the attention coefficients).
+ *   dropout_p  in [0, 1]; coefficient (CSR position k, head h) is kept iff
+ *              hash(seed, k*heads + h) >= round(dropout_p * 2^32) and then scaled
+ *              by 1/(1 - dropout_p); the softmax denominator is not dropped.
+ *              The mask is a pure function of (seed, k, h): the backward
+ *              regenerates it from the same seed.
+ *   lse        [rows, heads] REQUIRED: log-sum-exp per (row, head)
+ *   y_heads    [rows, heads*f] REQUIRED: per-head aggregation sum_k A_k Wh[j_k]
+ *              (after dropout, before head mean and bias)
+ * Other arguments as gat_edge_aggregate.
+ */
+int gat_edge_aggregate_train(const int* rowptr, const int* col, const int* row_order,
+                             int row_begin, int row_end, const float* wh, int ld_wh,
+                             const float* s_src, int ld_s, const float* a_src, const float* c_src,
+                             const float* s_dst, int heads, int f, int concat,
+                             float negative_slope, float dropout_p, unsigned long long seed,
+                             const float* bias, float* out, float* lse, float* y_heads,
+                             int edges_per_row_hint, void* stream);
+
+/* Workspace bytes gat_csc_build needs for nnz = E + N CSR entries. */
+int gat_csc_workspace_size(long long nnz, int num_nodes, size_t* bytes);
+
+/*
+ * Transpose of the CSR (edges grouped by SOURCE), for the backward pass.
+ *   rowptr/col  from gat_csr_build; nnz = rowptr[num_nodes]
+ *   csc_ptr     [num_nodes + 1] int32: first CSC slot of each source node
+ *   csc_dst     [nnz] int32: target row of the edge in each CSC slot
+ *   csr_to_csc  [nnz] int32: CSC slot of each CSR position
+ * Within a source, slots follow CSR order (stable), so reductions over them are
+ * deterministic.
+ */
+int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nnz, int* csc_ptr,
+                  int* csc_dst, int* csr_to_csc, void* workspace, size_t workspace_bytes,
+                  void* stream);
+
+/*
+ * Backward pass 1, per TARGET row (softmax + LeakyReLU + dropout backward).
+ *   grad_out   dL/d(layer output) [rows, heads*f] (concat) or [rows, f] (mean)
+ *   lse, y_heads  as written by gat_edge_aggregate_train (same seed / dropout_p)
+ *   s_src      as written by gat_project
+ * Writes:
+ *   ds_dst     [rows, heads]  dL/ds_dst
+ *   alpha_csc  [nnz, heads]   coefficient used in the forward (after dropout), at
+ *                             each edge's CSC slot
+ *   dz_csc     [nnz, heads]   dL/d(s_dst[i] + s_src[j]) per edge, at its CSC slot
+ */
+int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_order,
+                           int row_begin, int row_end, const int* csr_to_csc, const float* wh,
+                           int ld_wh, const float* s_src, int ld_s, const float* s_dst,
+                           const float* lse, const float* y_heads, const float* grad_out,
+                           int heads, int f, int concat, float negative_slope, float dropout_p,
+                           unsigned long long seed, float* ds_dst, float* alpha_csc,
+                           float* dz_csc, void* stream);
+
+/*
+ * Backward pass 2, per SOURCE row: message backward plus the score terms.
+ *   dwh[j]     = sum_{edges j->i} alpha * dy[i]  +  ds_src[j,h] a_src_h + ds_dst[j,h] a_dst_h
+ *                ([num_nodes, ld_dwh], columns [0, heads*f)) = dL/dWh
+ *   ds_src     optional [num_nodes, heads] = dL/ds_src
+ *   partials   [num_parts, 2*heads*f + 2*heads]: per-part sums of
+ *              [ds_src*Wh (da_src) | ds_dst*Wh (da_dst) | ds_src (dc_src) | ds_dst (dc_dst)];
+ *              the caller sums them over parts (deterministic, no atomics).
+ *   num_parts  >= 1; rows are strided over parts (a good value: min(num_nodes, 8192))
+ */
+int gat_src_backward(const int* csc_ptr, const int* csc_dst, int num_nodes, const float* wh,
+                     int ld_wh, const float* grad_out, const float* alpha_csc,
+                     const float* dz_csc, const float* ds_dst, const float* a_src,
+                     const float* a_dst, int heads, int f, int concat, float* dwh, int ld_dwh,
+                     float* ds_src, float* partials, int num_parts, void* stream);
 
 #ifdef __cplusplus
 }

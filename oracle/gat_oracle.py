@@ -54,6 +54,9 @@ __all__ = [
     "gat_layer_forward_from_state",
     "closed_form_forward",
     "init_reference_params",
+    "gat_layer_forward_differentiable",
+    "dropout_factors",
+    "csr_positions",
 ]
 
 
@@ -83,9 +86,12 @@ def segment_softmax(src: torch.Tensor, index: torch.Tensor, num_nodes: int) -> t
 
 
 def propagate(edge_index: torch.Tensor, x: torch.Tensor, attention_vals, num_nodes: int,
-              concat: bool, negative_slope: float = 0.2) -> torch.Tensor:
+              concat: bool, negative_slope: float = 0.2,
+              drop: Optional[torch.Tensor] = None) -> torch.Tensor:
     """PyG ``MessagePassing.propagate`` (``aggr='add'``, ``node_dim=0``) around
-    ``GAT.py:56-67``'s ``message`` in eval mode."""
+    ``GAT.py:56-67``'s ``message``.  ``drop`` ([E, H] multipliers, 0 or
+    1/(1-p)) applies ``GAT.py:61``'s training-mode dropout with a given mask;
+    None is eval mode."""
     src, dst = edge_index[0], edge_index[1]
     # __collect__: _j lifts with edge_index[0] and takes tuple element 0,
     #              _i lifts with edge_index[1] and takes tuple element 1.
@@ -96,6 +102,8 @@ def propagate(edge_index: torch.Tensor, x: torch.Tensor, attention_vals, num_nod
     e = att_i + att_j
     e = torch.nn.functional.leaky_relu(e, negative_slope)
     alpha = segment_softmax(e, dst, num_nodes)
+    if drop is not None:
+        alpha = alpha * drop
     out = x_j * alpha.view(alpha.shape[0], alpha.shape[1], 1)
     if concat:
         out = out.reshape(out.shape[0], -1)
@@ -216,3 +224,76 @@ def init_reference_params(input_channels: int, output_channels: int, num_heads: 
             state[f"{name}.{h}.weight"] = m.weight.detach().clone()
             state[f"{name}.{h}.bias"] = m.bias.detach().clone()
     return state
+
+
+def gat_layer_forward_differentiable(params: Dict[str, torch.Tensor], x: torch.Tensor,
+                                     edge_index: torch.Tensor, num_heads: int, concat: bool,
+                                     negative_slope: float = 0.2,
+                                     drop: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``GAT.py:37-67`` with autograd left on (the reference trains through
+    it with ``loss.backward()``): the gradient oracle.  ``params`` uses the
+    reference ``state_dict`` keys; ``drop`` is the dropout multiplier per
+    (edge in add_self_loops order, head)."""
+    H = num_heads
+    n = x.size(0)
+    edge_ind = add_self_loops(edge_index, n)
+    transformed, a1s, a2s = [], [], []
+    for h in range(H):
+        t = torch.nn.functional.linear(x, params[f"ws.{h}.weight"], params[f"ws.{h}.bias"])
+        transformed.append(t)
+        a1s.append(torch.nn.functional.linear(t, params[f"attentions1.{h}.weight"],
+                                              params[f"attentions1.{h}.bias"]))
+        a2s.append(torch.nn.functional.linear(t, params[f"attentions2.{h}.weight"],
+                                              params[f"attentions2.{h}.bias"]))
+    transformed = torch.transpose(torch.stack(transformed), 0, 1)
+    a1 = torch.stack(a1s).squeeze(-1).T
+    a2 = torch.stack(a2s).squeeze(-1).T
+    return propagate(edge_ind, transformed, (a1, a2), n, concat, negative_slope,
+                     drop) + params["bias"]
+
+
+def _mix32(x):
+    import numpy as np
+    x = x.astype(np.uint32)
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def dropout_factors(positions, num_heads: int, p: float, seed: int):
+    """The HIP library's attention-dropout mask, restated in numpy (its
+    ``drop_factor``: keep (k, h) iff mix(seed, k*H + h) >= round(p * 2^32)).
+    ``positions`` are CSR edge positions; returns float64 [len, H] of 0 or
+    1/(1-p).  The mask itself is a design choice of this library (the
+    reference draws it from torch's RNG, GAT.py:61), so parity of a dropout
+    step is checked against this mask, not the reference's draw."""
+    import numpy as np
+    k = np.asarray(positions, dtype=np.uint64)[:, None]
+    h = np.arange(num_heads, dtype=np.uint64)[None, :]
+    idx = k * np.uint64(num_heads) + h
+    lo = (idx & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    hi = (idx >> np.uint64(32)).astype(np.uint32)
+    seed_lo = np.uint32(seed & 0xFFFFFFFF)
+    seed_hi = np.uint32((seed >> 32) & 0xFFFFFFFF)
+    a = _mix32(lo ^ seed_lo)
+    with np.errstate(over="ignore"):
+        b = _mix32((hi + seed_hi).astype(np.uint32))
+    r = _mix32(a ^ b)
+    thresh = min(max(math.floor(p * 4294967296.0 + 0.5), 0), 4294967295)
+    scale = 1.0 if p <= 0 else (0.0 if p >= 1 else
+                                 float(np.float32(1.0) / (np.float32(1.0) - np.float32(p))))
+    return np.where(r >= np.uint32(thresh), scale, 0.0)
+
+
+def csr_positions(edge_index: torch.Tensor, num_nodes: int):
+    """CSR position of each edge of ``add_self_loops(edge_index)`` in the HIP
+    library's CSR (stable sort by target, loops last per row)."""
+    import numpy as np
+    dst = np.concatenate([edge_index[1].cpu().numpy(), np.arange(num_nodes)])
+    order = np.argsort(dst, kind="stable")
+    pos = np.empty_like(order)
+    pos[order] = np.arange(order.size)
+    return pos

@@ -50,3 +50,35 @@ def test_src_dst_convention():
             st[f"attentions2.{h}.bias"], st[f"attentions1.{h}.bias"])
     swapped = gat_layer_forward_from_state(st, g["x"], g["edge_index"], m["H"], m["concat"])
     assert not torch.allclose(swapped, g["out"], atol=1e-4)
+
+
+def test_differentiable_oracle_matches_fixture_and_has_grads():
+    """gat_layer_forward_differentiable (the gradient oracle) equals the
+    fixture-pinned forward, and autograd reaches every parameter."""
+    import torch
+    from oracle import gat_layer_forward_differentiable
+    g = load_golden("grid_h4_f8_cat")
+    meta = g["meta"]
+    params = {k: v.double().requires_grad_(True) for k, v in g["state"].items()}
+    out = gat_layer_forward_differentiable(params, g["x"].double(), g["edge_index"],
+                                           meta["H"], meta["concat"])
+    assert torch.allclose(out.float(), g["out"], atol=1e-5, rtol=0)
+    out.sum().backward()
+    assert all(p.grad is not None for p in params.values())
+
+
+def test_dropout_mask_restatement_properties():
+    import numpy as np
+    from oracle import csr_positions, dropout_factors
+    m = dropout_factors(np.arange(200000), 8, 0.6, 7)
+    assert abs((m > 0).mean() - 0.4) < 0.005
+    assert np.allclose(m[m > 0], 2.5)
+    assert (dropout_factors(np.arange(1000), 4, 0.0, 7) == 1.0).all()
+    assert (dropout_factors(np.arange(1000), 4, 1.0, 7) == 0.0).all()
+    # different seeds and heads decorrelate
+    m2 = dropout_factors(np.arange(200000), 8, 0.6, 8)
+    assert abs(((m > 0) == (m2 > 0)).mean() - 0.52) < 0.01
+    # CSR positions: stable by target, loops last per row
+    import torch
+    ei = torch.tensor([[1, 2, 0], [1, 0, 1]])
+    assert csr_positions(ei, 3).tolist() == [2, 0, 3, 1, 4, 5]
