@@ -6,7 +6,9 @@ danieldritter/ATMLGraphAttentionNetworks (``GAT.py:GraphAttentionLayer``).
 PyTorch-ROCm host code over the C-ABI HIP library ``libgat_amd.so``
 (``include/gat_amd.h``).  See DESIGN.md / INTEGRATION.md.
 """
-from .layer import GraphAttentionLayer, gat_forward, pack_params  # noqa: F401
+from .layer import (GraphAttentionLayer, GraphAttentionLayerActivationTest,  # noqa: F401
+                    gat_forward, pack_params)
 from .graph import CSRGraph, build_csr, get_csr  # noqa: F401
 
-__all__ = ["GraphAttentionLayer", "gat_forward", "pack_params", "CSRGraph", "build_csr", "get_csr"]
+__all__ = ["GraphAttentionLayer", "GraphAttentionLayerActivationTest", "gat_forward",
+           "pack_params", "CSRGraph", "build_csr", "get_csr"]

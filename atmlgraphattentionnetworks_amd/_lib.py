@@ -20,6 +20,10 @@ GAT_EWORKSPACE = -3
 GAT_ABI_VERSION = 2
 GAT_MAX_HEADS = 64
 GAT_MAX_HF = 256
+GAT_ACT_LEAKY_RELU = 0
+GAT_ACT_LOG_SIGMOID = 1
+GAT_ACT_TANH = 2
+GAT_ACT_HEAD_SOFTMAX = 3
 
 _c_int, _c_ll, _c_float, _c_vp = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -38,17 +42,17 @@ SIGNATURES = {
     "gat_csr_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csr_build": (_c_int, [_c_vp, _c_ll, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, ctypes.c_size_t,
                                _c_vp, _c_vp]),
-    "gat_edge_aggregate_train": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
-                                          _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
-                                          _c_int, _c_float, _c_float, _c_u64, _c_vp, _c_vp,
-                                          _c_vp, _c_vp, _c_int, _c_vp]),
+    "gat_edge_aggregate_ex": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
+                                       _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
+                                       _c_int, _c_int, _c_float, _c_float, _c_u64, _c_vp, _c_vp,
+                                       _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_csc_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csc_build": (_c_int, [_c_vp, _c_vp, _c_int, _c_ll, _c_vp, _c_vp, _c_vp, _c_vp,
                                ctypes.c_size_t, _c_vp]),
     "gat_edge_backward_rows": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp,
                                         _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
-                                        _c_int, _c_int, _c_int, _c_float, _c_float, _c_u64,
-                                        _c_vp, _c_vp, _c_vp, _c_vp]),
+                                        _c_int, _c_int, _c_int, _c_int, _c_float, _c_float,
+                                        _c_u64, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gat_src_backward": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
                                   _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int,
                                   _c_vp, _c_vp, _c_int, _c_vp]),

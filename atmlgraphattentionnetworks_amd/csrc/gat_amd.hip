@@ -49,6 +49,45 @@ __device__ __forceinline__ float leaky(float z, float slope) {
     return z > 0.f ? z : z * slope;
 }
 
+// Score activations (GAT.py:30 LeakyReLU; run_act_func_experiment.py:111
+// LogSigmoid, Tanh, Softmax — the last with torch's implicit dim=1 on the
+// [E', H] scores, i.e. a softmax across the heads of each edge).
+__device__ __forceinline__ float score_act(int act, float z, float param) {
+    if (act == GAT_ACT_LOG_SIGMOID) return fminf(z, 0.f) - log1pf(expf(-fabsf(z)));
+    if (act == GAT_ACT_TANH) return tanhf(z);
+    return leaky(z, param);
+}
+
+// d act / dz for the elementwise activations
+__device__ __forceinline__ float score_act_grad(int act, float z, float param) {
+    if (act == GAT_ACT_LOG_SIGMOID) return 1.f / (1.f + expf(z));  // sigmoid(-z)
+    if (act == GAT_ACT_TANH) {
+        const float t = tanhf(z);
+        return 1.f - t * t;
+    }
+    return z > 0.f ? 1.f : param;
+}
+
+// softmax over the HP consecutive lanes holding one edge's heads
+template <int HP>
+__device__ __forceinline__ float head_softmax(float z, bool valid) {
+    float m = valid ? z : -INFINITY;
+#pragma unroll
+    for (int off = 1; off < HP; off <<= 1) m = fmaxf(m, __shfl_xor(m, off));
+    const float p = valid ? expf(z - m) : 0.f;
+    float sum = p;
+#pragma unroll
+    for (int off = 1; off < HP; off <<= 1) sum += __shfl_xor(sum, off);
+    return valid ? p / sum : 0.f;
+}
+
+template <int HP>
+__device__ __forceinline__ float head_sum(float v) {
+#pragma unroll
+    for (int off = 1; off < HP; off <<= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
 __host__ __device__ constexpr int round_up4(int v) { return (v + 3) & ~3; }
 
 // Attention dropout (GAT.py:61, F.dropout on the softmax coefficients, training
@@ -575,7 +614,7 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
     int row_begin, int row_end,
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
     const float* __restrict__ s_dst,
-    int H, int F, int HF, int concat, float slope, const float* __restrict__ bias,
+    int H, int F, int HF, int concat, int act, float slope, const float* __restrict__ bias,
     float* __restrict__ out, int ld_out, float* __restrict__ lse, DropArgs drop,
     float* __restrict__ y_heads) {
     constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;  // edges per chunk
@@ -622,11 +661,12 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int k = (lane + kWave * q) / HP;
-            float e = -INFINITY;
-            if (k < nk && hs_ok) {
-                const int j = col_s[k];
-                e = leaky(sd + Ss[(size_t)j * ld_s + hs], slope);
-            }
+            const bool valid = k < nk && hs_ok;
+            const int j = col_s[k < nk ? k : nk - 1];
+            const float z = sd + Ss[(size_t)j * ld_s + (hs_ok ? hs : 0)];
+            float e = act == GAT_ACT_HEAD_SOFTMAX ? head_softmax<HP>(z, valid)
+                                                  : score_act(act, z, slope);
+            e = valid ? e : -INFINITY;
             ev[q] = e;
             mloc = fmaxf(mloc, e);
         }
@@ -1010,7 +1050,7 @@ __global__ __launch_bounds__(64) void k_edge_bwd_rows(
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
     const float* __restrict__ s_dst, const float* __restrict__ lse,
     const float* __restrict__ y_heads, const float* __restrict__ g, int H, int F, int HF,
-    int concat, float slope, DropArgs drop, float* __restrict__ ds_dst,
+    int concat, int act, float slope, DropArgs drop, float* __restrict__ ds_dst,
     float* __restrict__ alpha_out, float* __restrict__ dz_out) {
     constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;
     constexpr int R = C * HP / kWave;
@@ -1052,16 +1092,28 @@ __global__ __launch_bounds__(64) void k_edge_bwd_rows(
 #pragma unroll
         for (int q = 0; q < R; ++q) {
             const int k = (lane + kWave * q) / HP;
-            if (k < nk && hs_ok) {
-                const int j = col_s[k];
-                const float z = sd + Ss[(size_t)j * ld_s + hs];
-                const float a = expf(leaky(z, slope) - ls);
+            const bool valid = k < nk && hs_ok;
+            const int j = col_s[k < nk ? k : nk - 1];
+            const float z = sd + Ss[(size_t)j * ld_s + (hs_ok ? hs : 0)];
+            const bool hsm = act == GAT_ACT_HEAD_SOFTMAX;
+            const float ev = hsm ? head_softmax<HP>(z, valid) : score_act(act, z, slope);
+            float de = 0.f, a = 0.f, dm = 1.f;
+            if (valid) {
+                a = expf(ev - ls);
                 const float* wr = Wh + (size_t)j * ld_wh + hs * F;
                 float da = 0.f;
                 for (int f = 0; f < F; ++f) da = fmaf(dyh[f], wr[f], da);
-                const float dm = drop.thresh != 0u ? drop_factor(drop, base + k, hs, H) : 1.f;
-                const float de = a * (dm * da - dl);
-                const float dz = z > 0.f ? de : de * slope;
+                if (drop.thresh != 0u) dm = drop_factor(drop, base + k, hs, H);
+                de = a * (dm * da - dl);
+            }
+            float dz;
+            if (hsm) {  // d softmax_h: e_h (de_h - sum_h' e_h' de_h')
+                const float sum = head_sum<HP>(ev * de);
+                dz = ev * (de - sum);
+            } else {
+                dz = de * score_act_grad(act, z, slope);
+            }
+            if (valid) {
                 dsd += dz;
                 const size_t o = (size_t)slot_s[k] * H + hs;
                 alpha_out[o] = a * dm;
@@ -1347,9 +1399,10 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
                                int row_begin, int row_end, const float* wh, int ld_wh,
                                const float* s_src, int ld_s, const float* a_src,
                                const float* c_src, const float* s_dst, int heads, int f,
-                               int concat, float negative_slope, const float* bias, float* out,
-                               float* lse, float* y_heads, DropArgs drop,
+                               int concat, int act, float negative_slope, const float* bias,
+                               float* out, float* lse, float* y_heads, DropArgs drop,
                                int edges_per_row_hint, void* stream) {
+    if (act < GAT_ACT_LEAKY_RELU || act > GAT_ACT_HEAD_SOFTMAX) return GAT_EINVAL;
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
@@ -1361,7 +1414,9 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
     if (rows == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
     const int ld_out = concat ? hf : f;
-    const bool slope_ok = negative_slope >= 0.f && negative_slope <= 1.f;
+    // the lane-group kernel computes LeakyReLU as max(z, slope*z)
+    const bool slope_ok = act == GAT_ACT_LEAKY_RELU && negative_slope >= 0.f &&
+                          negative_slope <= 1.f;
     // V float4s per lane (one head per lane needs f % 4V == 0): fewer, fuller
     // waves; GAT_EDGE_V overrides
     const bool dropping = drop.thresh != 0u;
@@ -1433,7 +1488,7 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
 #define GAT_EDGE_LAUNCH(L, P)                                                                \
     hipLaunchKernelGGL((k_edge_fwd<L, P>), grid, block, 0, st, rowptr, col, row_order,       \
                        row_begin,                                                            \
-                       row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat,         \
+                       row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat, act,    \
                        negative_slope, bias, out, ld_out, lse, drop, y_heads)
 #define GAT_EDGE_HP(L)                                                                       \
     switch (hp) {                                                                            \
@@ -1467,24 +1522,22 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
                        int f, int concat, float negative_slope, const float* bias, float* out,
                        float* lse, int edges_per_row_hint, void* stream) {
     return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src,
-                               ld_s, a_src, c_src, s_dst, heads, f, concat, negative_slope, bias,
-                               out, lse, nullptr, make_drop(0.f, 0ull), edges_per_row_hint,
-                               stream);
+                               ld_s, a_src, c_src, s_dst, heads, f, concat, GAT_ACT_LEAKY_RELU,
+                               negative_slope, bias, out, lse, nullptr, make_drop(0.f, 0ull),
+                               edges_per_row_hint, stream);
 }
 
-int gat_edge_aggregate_train(const int* rowptr, const int* col, const int* row_order,
-                             int row_begin, int row_end, const float* wh, int ld_wh,
-                             const float* s_src, int ld_s, const float* a_src, const float* c_src,
-                             const float* s_dst, int heads, int f, int concat,
-                             float negative_slope, float dropout_p, unsigned long long seed,
-                             const float* bias, float* out, float* lse, float* y_heads,
-                             int edges_per_row_hint, void* stream) {
-    if (lse == nullptr || y_heads == nullptr) return GAT_EINVAL;
+int gat_edge_aggregate_ex(const int* rowptr, const int* col, const int* row_order, int row_begin,
+                          int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
+                          const float* a_src, const float* c_src, const float* s_dst, int heads,
+                          int f, int concat, int score_act, float act_param, float dropout_p,
+                          unsigned long long seed, const float* bias, float* out, float* lse,
+                          float* y_heads, int edges_per_row_hint, void* stream) {
     if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
     return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src,
-                               ld_s, a_src, c_src, s_dst, heads, f, concat, negative_slope, bias,
-                               out, lse, y_heads, make_drop(dropout_p, seed), edges_per_row_hint,
-                               stream);
+                               ld_s, a_src, c_src, s_dst, heads, f, concat, score_act, act_param,
+                               bias, out, lse, y_heads, make_drop(dropout_p, seed),
+                               edges_per_row_hint, stream);
 }
 
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes) {
@@ -1594,9 +1647,10 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
                            int row_begin, int row_end, const int* csr_to_csc, const float* wh,
                            int ld_wh, const float* s_src, int ld_s, const float* s_dst,
                            const float* lse, const float* y_heads, const float* grad_out,
-                           int heads, int f, int concat, float negative_slope, float dropout_p,
-                           unsigned long long seed, float* ds_dst, float* alpha_csc,
-                           float* dz_csc, void* stream) {
+                           int heads, int f, int concat, int score_act, float act_param,
+                           float dropout_p, unsigned long long seed, float* ds_dst,
+                           float* alpha_csc, float* dz_csc, void* stream) {
+    if (score_act < GAT_ACT_LEAKY_RELU || score_act > GAT_ACT_HEAD_SOFTMAX) return GAT_EINVAL;
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
@@ -1611,7 +1665,8 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
     case P:                                                                                   \
         hipLaunchKernelGGL((k_edge_bwd_rows<P>), grid, block, 0, st, rowptr, col, row_order,  \
                            row_begin, row_end, csr_to_csc, wh, ld_wh, s_src, ld_s, s_dst, lse, \
-                           y_heads, grad_out, heads, f, hf, concat, negative_slope, drop,     \
+                           y_heads, grad_out, heads, f, hf, concat, score_act, act_param,     \
+                           drop,                                                              \
                            ds_dst, alpha_csc, dz_csc);                                        \
         break;
     switch (next_pow2(heads)) {

@@ -28,7 +28,8 @@ import torch
 from . import _lib
 from .graph import CSRGraph, get_csr
 
-__all__ = ["GraphAttentionLayer", "PackedParams", "pack_params", "gat_forward", "NodeTable",
+__all__ = ["GraphAttentionLayer", "GraphAttentionLayerActivationTest", "score_activation_code",
+           "PackedParams", "pack_params", "gat_forward", "NodeTable",
            "alloc_table", "project", "edge_aggregate"]
 
 
@@ -188,6 +189,32 @@ def gat_forward(x: torch.Tensor, csr: CSRGraph, pp: PackedParams, bias: torch.Te
     return out
 
 
+def score_activation_code(module) -> Tuple[int, float]:
+    """Map the layer's ``attention_relu`` module to the library's score
+    activation (``GAT_ACT_*``, parameter).  The reference uses
+    ``LeakyReLU(0.2)`` (``GAT.py:30``); its activation experiment swaps in
+    ``LogSigmoid``, ``Tanh`` and ``Softmax()`` (``run_act_func_experiment.py:111``),
+    the last with torch's implicit ``dim=1`` on the 2-D ``[E', H]`` scores."""
+    if isinstance(module, torch.nn.LeakyReLU):
+        return _lib.GAT_ACT_LEAKY_RELU, float(module.negative_slope)
+    if isinstance(module, torch.nn.ReLU):
+        return _lib.GAT_ACT_LEAKY_RELU, 0.0
+    if isinstance(module, torch.nn.Identity):
+        return _lib.GAT_ACT_LEAKY_RELU, 1.0
+    if isinstance(module, torch.nn.LogSigmoid):
+        return _lib.GAT_ACT_LOG_SIGMOID, 0.0
+    if isinstance(module, torch.nn.Tanh):
+        return _lib.GAT_ACT_TANH, 0.0
+    if isinstance(module, torch.nn.Softmax):
+        if module.dim in (None, 1, -1):
+            return _lib.GAT_ACT_HEAD_SOFTMAX, 0.0
+        raise NotImplementedError(
+            f"Softmax(dim={module.dim}) over the edge scores is not supported (dim=1: across heads)")
+    raise NotImplementedError(
+        f"score activation {type(module).__name__} is not supported by the HIP kernels "
+        "(LeakyReLU, ReLU, Identity, LogSigmoid, Tanh, Softmax(dim=1))")
+
+
 def _check_x(x: torch.Tensor, in_channels: int) -> torch.Tensor:
     if not isinstance(x, torch.Tensor):
         raise TypeError(f"x must be a torch.Tensor, got {type(x).__name__}")
@@ -239,6 +266,11 @@ class GraphAttentionLayer(torch.nn.Module):
     def negative_slope(self) -> float:
         return float(self.attention_relu.negative_slope)
 
+    def score_activation(self) -> Tuple[int, float]:
+        """(GAT_ACT_*, parameter) of ``self.attention_relu`` (read per call, so
+        replacing the module after construction takes effect as in the reference)."""
+        return score_activation_code(self.attention_relu)
+
     def packed(self) -> PackedParams:
         self._packed = pack_params(self, self._packed)
         return self._packed
@@ -249,14 +281,31 @@ class GraphAttentionLayer(torch.nn.Module):
         p = float(self.dropout_val) if self.training else 0.0
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or any(p_.requires_grad for p_ in self.parameters()))
-        if needs_grad or p > 0.0:
+        act, act_param = self.score_activation()
+        default_act = act == _lib.GAT_ACT_LEAKY_RELU and 0.0 <= act_param <= 1.0
+        if needs_grad or p > 0.0 or not default_act:
             # training path (training.py): dropout of GAT.py:61 and the HIP backward
             from .training import gat_train_forward, new_dropout_seed
             seed = new_dropout_seed() if p > 0.0 else 0
             return gat_train_forward(self, x, csr, p, seed)
         return gat_forward(x, csr, self.packed(), self.bias.detach(), self.num_heads,
-                           self.output_channels, self.concat, self.negative_slope)
+                           self.output_channels, self.concat, act_param)
 
     def extra_repr(self) -> str:
         return (f"{self.input_channels}, {self.output_channels}, num_heads={self.num_heads}, "
                 f"concat={self.concat}, dropout={self.dropout_val}")
+
+
+class GraphAttentionLayerActivationTest(GraphAttentionLayer):
+    """Counterpart of ``run_act_func_experiment.py:13``: the same layer with the
+    score activation passed in (``activation_function``, default LeakyReLU(0.2)).
+    Supported: LeakyReLU, ReLU, Identity, LogSigmoid, Tanh, Softmax(dim=1)."""
+
+    def __init__(self, input_channels, output_channels, num_heads=1, concat=False, dropout=0.6,
+                 activation_function=None):
+        super().__init__(input_channels, output_channels, num_heads=num_heads, concat=concat,
+                         dropout=dropout)
+        if activation_function is None:
+            activation_function = torch.nn.LeakyReLU(negative_slope=0.2)
+        score_activation_code(activation_function)  # fail at construction if unsupported
+        self.attention_relu = activation_function

@@ -6,8 +6,9 @@ PyG's gather/scatter ops (``run_inductive.py:83-90``, ``run_*_experiment.py``:
 ``loss.backward(); optimizer.step()``).  Here the gradient of
 ``GAT.py:37-67`` is computed by three library calls and two plain GEMMs:
 
-  forward   gat_project, then gat_edge_aggregate_train (dropout GAT.py:61 from a
-            counter-based hash; also stores lse and the per-head aggregation y)
+  forward   gat_project, then gat_edge_aggregate_ex (dropout GAT.py:61 from a
+            counter-based hash; any score activation; also stores lse and the
+            per-head aggregation y)
   backward  1. gat_edge_backward_rows (per target row: dropout, softmax and
                LeakyReLU backward -> ds_dst, and per-edge A / dz in CSC order)
             2. gat_src_backward (per source row: dWh = sum A * dy + the score
@@ -43,7 +44,7 @@ class GATFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, a_src, c_src, a_dst, c_dst, bias, csr: CSRGraph, heads: int,
-                f: int, concat: bool, slope: float, p: float, seed: int):
+                f: int, concat: bool, act: int, act_param: float, p: float, seed: int):
         lib = _lib.load()
         n, fin = x.shape
         hf = heads * f
@@ -62,22 +63,23 @@ class GATFunction(torch.autograd.Function):
         lse = torch.empty(n, heads, dtype=torch.float32, device=dev)
         y = torch.empty(n, hf, dtype=torch.float32, device=dev)
         order = csr.order
-        _lib.check(lib.gat_edge_aggregate_train(
+        _lib.check(lib.gat_edge_aggregate_ex(
             csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
             0, n, wh.data_ptr(), hfp, s_src.data_ptr(), heads, a_src.data_ptr(),
-            c_src.data_ptr(), s_dst.data_ptr(), heads, f, int(concat), float(slope), float(p),
-            int(seed), bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(),
-            csr.num_edges // max(n, 1), stream), "gat_edge_aggregate_train")
+            c_src.data_ptr(), s_dst.data_ptr(), heads, f, int(concat), int(act),
+            float(act_param), float(p), int(seed), bias.data_ptr(), out.data_ptr(),
+            lse.data_ptr(), y.data_ptr(), csr.num_edges // max(n, 1), stream),
+            "gat_edge_aggregate_ex")
         ctx.save_for_backward(x, w, a_src, a_dst, wh, s_src, s_dst, lse, y)
         ctx.csr = csr
-        ctx.cfg = (heads, f, bool(concat), float(slope), float(p), int(seed))
+        ctx.cfg = (heads, f, bool(concat), int(act), float(act_param), float(p), int(seed))
         return out
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, g):
         x, w, a_src, a_dst, wh, s_src, s_dst, lse, y = ctx.saved_tensors
-        heads, f, concat, slope, p, seed = ctx.cfg
+        heads, f, concat, act, act_param, p, seed = ctx.cfg
         csr = ctx.csr
         lib = _lib.load()
         g = g.contiguous()
@@ -98,7 +100,7 @@ class GATFunction(torch.autograd.Function):
             csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
             0, n, csc.csr_to_csc.data_ptr(), wh.data_ptr(), hfp, s_src.data_ptr(), heads,
             s_dst.data_ptr(), lse.data_ptr(), y.data_ptr(), g.data_ptr(), heads, f, int(concat),
-            slope, p, seed, ds_dst.data_ptr(), alpha.data_ptr(), dz.data_ptr(), stream),
+            act, act_param, p, seed, ds_dst.data_ptr(), alpha.data_ptr(), dz.data_ptr(), stream),
             "gat_edge_backward_rows")
         parts = max(1, min(n, _MAX_PARTS))
         dwh = torch.empty(n, hf, dtype=torch.float32, device=dev)
@@ -119,7 +121,7 @@ class GATFunction(torch.autograd.Function):
         dc_dst = ps[2 * hf + heads:] if need[6] else None
         dbias = g.sum(0) if need[7] else None
         return (dx, dw, db, da_src, dc_src, da_dst, dc_dst, dbias,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def packed_params_differentiable(layer):
@@ -140,6 +142,7 @@ def packed_params_differentiable(layer):
 
 def gat_train_forward(layer, x: torch.Tensor, csr: CSRGraph, p: float, seed: int):
     w, b, a_src, c_src, a_dst, c_dst = packed_params_differentiable(layer)
+    act, act_param = layer.score_activation()
     return GATFunction.apply(x, w, b, a_src, c_src, a_dst, c_dst, layer.bias, csr,
                              layer.num_heads, layer.output_channels, layer.concat,
-                             layer.negative_slope, p, seed)
+                             act, act_param, p, seed)

@@ -39,6 +39,12 @@ extern "C" {
 #define GAT_EWORKSPACE (-3)   /* workspace smaller than gat_csr_workspace_size      */
 
 #define GAT_MAX_HEADS 64 /* num_heads                    */
+
+/* Score activations (the attention_relu module, GAT.py:30 / run_act_func_experiment.py:111) */
+#define GAT_ACT_LEAKY_RELU 0   /* LeakyReLU(act_param), the reference default 0.2          */
+#define GAT_ACT_LOG_SIGMOID 1  /* LogSigmoid                                                */
+#define GAT_ACT_TANH 2         /* Tanh                                                      */
+#define GAT_ACT_HEAD_SOFTMAX 3 /* Softmax(dim=1) on the [E', heads] scores: across heads    */
 #define GAT_MAX_HF 256   /* num_heads * output_channels  */
 
 /* ABI version of the loaded library (== GAT_ABI_VERSION). */
@@ -135,25 +141,28 @@ int gat_csr_build(const long long* edge_index, long long num_edges, int num_node
  * ------------------------------------------------------------------------- */
 
 /*
- * gat_edge_aggregate plus what the backward needs.  Replaces GAT.py:53-67 in
- * training mode, including GAT.py:61 (F.dropout on the attention coefficients).
+ * gat_edge_aggregate generalised: any score activation, attention dropout, and
+ * the tensors the backward needs.  Replaces GAT.py:53-67 in training mode,
+ * including GAT.py:61 (F.dropout on the attention coefficients), and the
+ * activation experiment's layer (run_act_func_experiment.py:13-74).
+ *   score_act  GAT_ACT_*; act_param is the LeakyReLU slope (ignored otherwise).
+ *              Only LeakyReLU with slope in [0, 1] uses the lane-group kernel.
  *   dropout_p  in [0, 1]; coefficient (CSR position k, head h) is kept iff
  *              hash(seed, k*heads + h) >= round(dropout_p * 2^32) and then scaled
  *              by 1/(1 - dropout_p); the softmax denominator is not dropped.
  *              The mask is a pure function of (seed, k, h): the backward
  *              regenerates it from the same seed.
- *   lse        [rows, heads] REQUIRED: log-sum-exp per (row, head)
- *   y_heads    [rows, heads*f] REQUIRED: per-head aggregation sum_k A_k Wh[j_k]
+ *   lse        optional [rows, heads]: log-sum-exp per (row, head)
+ *   y_heads    optional [rows, heads*f]: per-head aggregation sum_k A_k Wh[j_k]
  *              (after dropout, before head mean and bias)
  * Other arguments as gat_edge_aggregate.
  */
-int gat_edge_aggregate_train(const int* rowptr, const int* col, const int* row_order,
-                             int row_begin, int row_end, const float* wh, int ld_wh,
-                             const float* s_src, int ld_s, const float* a_src, const float* c_src,
-                             const float* s_dst, int heads, int f, int concat,
-                             float negative_slope, float dropout_p, unsigned long long seed,
-                             const float* bias, float* out, float* lse, float* y_heads,
-                             int edges_per_row_hint, void* stream);
+int gat_edge_aggregate_ex(const int* rowptr, const int* col, const int* row_order, int row_begin,
+                          int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
+                          const float* a_src, const float* c_src, const float* s_dst, int heads,
+                          int f, int concat, int score_act, float act_param, float dropout_p,
+                          unsigned long long seed, const float* bias, float* out, float* lse,
+                          float* y_heads, int edges_per_row_hint, void* stream);
 
 /* Workspace bytes gat_csc_build needs for nnz = E + N CSR entries. */
 int gat_csc_workspace_size(long long nnz, int num_nodes, size_t* bytes);
@@ -174,7 +183,7 @@ int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nn
 /*
  * Backward pass 1, per TARGET row (softmax + LeakyReLU + dropout backward).
  *   grad_out   dL/d(layer output) [rows, heads*f] (concat) or [rows, f] (mean)
- *   lse, y_heads  as written by gat_edge_aggregate_train (same seed / dropout_p)
+ *   lse, y_heads  as written by gat_edge_aggregate_ex (same activation, seed, dropout_p)
  *   s_src      as written by gat_project
  * Writes:
  *   ds_dst     [rows, heads]  dL/ds_dst
@@ -186,9 +195,9 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
                            int row_begin, int row_end, const int* csr_to_csc, const float* wh,
                            int ld_wh, const float* s_src, int ld_s, const float* s_dst,
                            const float* lse, const float* y_heads, const float* grad_out,
-                           int heads, int f, int concat, float negative_slope, float dropout_p,
-                           unsigned long long seed, float* ds_dst, float* alpha_csc,
-                           float* dz_csc, void* stream);
+                           int heads, int f, int concat, int score_act, float act_param,
+                           float dropout_p, unsigned long long seed, float* ds_dst,
+                           float* alpha_csc, float* dz_csc, void* stream);
 
 /*
  * Backward pass 2, per SOURCE row: message backward plus the score terms.

@@ -87,11 +87,12 @@ def segment_softmax(src: torch.Tensor, index: torch.Tensor, num_nodes: int) -> t
 
 def propagate(edge_index: torch.Tensor, x: torch.Tensor, attention_vals, num_nodes: int,
               concat: bool, negative_slope: float = 0.2,
-              drop: Optional[torch.Tensor] = None) -> torch.Tensor:
+              drop: Optional[torch.Tensor] = None, activation=None) -> torch.Tensor:
     """PyG ``MessagePassing.propagate`` (``aggr='add'``, ``node_dim=0``) around
     ``GAT.py:56-67``'s ``message``.  ``drop`` ([E, H] multipliers, 0 or
     1/(1-p)) applies ``GAT.py:61``'s training-mode dropout with a given mask;
-    None is eval mode."""
+    None is eval mode.  ``activation`` replaces ``LeakyReLU(negative_slope)``
+    as the score activation module (``run_act_func_experiment.py:38,58``)."""
     src, dst = edge_index[0], edge_index[1]
     # __collect__: _j lifts with edge_index[0] and takes tuple element 0,
     #              _i lifts with edge_index[1] and takes tuple element 1.
@@ -100,7 +101,10 @@ def propagate(edge_index: torch.Tensor, x: torch.Tensor, attention_vals, num_nod
     att_i = attention_vals[1].index_select(0, dst)
     # message (GAT.py:57-66)
     e = att_i + att_j
-    e = torch.nn.functional.leaky_relu(e, negative_slope)
+    if activation is None:
+        e = torch.nn.functional.leaky_relu(e, negative_slope)
+    else:
+        e = activation(e)
     alpha = segment_softmax(e, dst, num_nodes)
     if drop is not None:
         alpha = alpha * drop
@@ -229,7 +233,8 @@ def init_reference_params(input_channels: int, output_channels: int, num_heads: 
 def gat_layer_forward_differentiable(params: Dict[str, torch.Tensor], x: torch.Tensor,
                                      edge_index: torch.Tensor, num_heads: int, concat: bool,
                                      negative_slope: float = 0.2,
-                                     drop: Optional[torch.Tensor] = None) -> torch.Tensor:
+                                     drop: Optional[torch.Tensor] = None,
+                                     activation=None) -> torch.Tensor:
     """``GAT.py:37-67`` with autograd left on (the reference trains through
     it with ``loss.backward()``): the gradient oracle.  ``params`` uses the
     reference ``state_dict`` keys; ``drop`` is the dropout multiplier per
@@ -249,7 +254,7 @@ def gat_layer_forward_differentiable(params: Dict[str, torch.Tensor], x: torch.T
     a1 = torch.stack(a1s).squeeze(-1).T
     a2 = torch.stack(a2s).squeeze(-1).T
     return propagate(edge_ind, transformed, (a1, a2), n, concat, negative_slope,
-                     drop) + params["bias"]
+                     drop, activation) + params["bias"]
 
 
 def _mix32(x):

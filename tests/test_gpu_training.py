@@ -217,3 +217,60 @@ def test_dropout_mask_matches_numpy_restatement():
     params = {k: v.double() for k, v in state.items()}
     ref = gat_layer_forward_differentiable(params, x.double(), ei, H, concat, drop=drop)
     _close("out", out, ref, 1e-5)
+
+
+ACTS = {
+    "log_sigmoid": lambda: torch.nn.LogSigmoid(),
+    "tanh": lambda: torch.nn.Tanh(),
+    "softmax": lambda: torch.nn.Softmax(),  # implicit dim=1 on [E', H]: across heads
+    "leaky_0.3": lambda: torch.nn.LeakyReLU(0.3),
+    "relu": lambda: torch.nn.ReLU(),
+    "leaky_neg": lambda: torch.nn.LeakyReLU(-0.5),  # outside [0, 1]: generic kernel
+}
+
+
+@pytest.mark.parametrize("act", sorted(ACTS))
+@pytest.mark.parametrize("case", [CASES[0], CASES[3], CASES[5]],
+                         ids=["H8F8_cat", "H1F7_mean", "H3F5_cat"])
+def test_score_activation_forward_and_backward(act, case):
+    """run_act_func_experiment.py's layer (activation_function argument):
+    eval forward, dropout forward and gradients against the oracle with the
+    same torch module applied to the [E', H] scores."""
+    import warnings
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayerActivationTest
+    n, e, fin, H, F, concat = case
+    _, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat, seed=4)
+    layer = GraphAttentionLayerActivationTest(fin, F, num_heads=H, concat=concat, dropout=0.0,
+                                              activation_function=ACTS[act]())
+    layer.load_state_dict(state)
+    layer = layer.to(DEV)
+    module = ACTS[act]()
+    gout = torch.randn(n, H * F if concat else F, generator=torch.Generator().manual_seed(8))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")  # Softmax's implicit-dim warning, as in the reference
+        params = {k: v.double() for k, v in state.items()}
+        ref = gat_layer_forward_differentiable(params, x.double(), ei, H, concat,
+                                               activation=module)
+        with torch.no_grad():
+            out = layer.eval()(x.to(DEV), ei.to(DEV))
+        _close("eval out", out, ref, 1e-5)
+        seed = 77
+        drop = torch.from_numpy(dropout_factors(csr_positions(ei, n), H, 0.3, seed))
+        xd, out = _run(layer.train(), x, ei, 0.3, seed)
+        layer.zero_grad()
+        (out * gout.to(DEV)).sum().backward()
+
+        def ref_grads(dtype):
+            ps = {k: v.to(dtype).clone().requires_grad_(True) for k, v in state.items()}
+            xr = x.to(dtype).clone().requires_grad_(True)
+            o = gat_layer_forward_differentiable(ps, xr, ei, H, concat, drop=drop.to(dtype),
+                                                 activation=module)
+            (o * gout.to(dtype)).sum().backward()
+            return o.detach(), xr.grad, {k: v.grad for k, v in ps.items()}
+        r_out, r_dx, r_dp = ref_grads(torch.float64)
+        _, s_dx, s_dp = ref_grads(torch.float32)
+    _close("train out", out, r_out, 1e-5)
+    _close("dx", xd.grad, r_dx, ref32=s_dx)
+    got = dict(layer.named_parameters())
+    for k, g in r_dp.items():
+        _close(k, got[k].grad, g, ref32=s_dp[k])

@@ -47,3 +47,31 @@ def test_cpu_tensor_raises_no_fallback():
     with pytest.raises(RuntimeError, match="no CPU path"):
         with torch.no_grad():
             layer(x, ei)
+
+
+def test_score_activation_codes():
+    import torch
+    from atmlgraphattentionnetworks_amd import _lib
+    from atmlgraphattentionnetworks_amd.layer import (GraphAttentionLayerActivationTest,
+                                                      score_activation_code)
+    assert score_activation_code(torch.nn.LeakyReLU(0.2)) == (_lib.GAT_ACT_LEAKY_RELU,
+                                                              pytest.approx(0.2))
+    assert score_activation_code(torch.nn.ReLU()) == (_lib.GAT_ACT_LEAKY_RELU, 0.0)
+    assert score_activation_code(torch.nn.LogSigmoid())[0] == _lib.GAT_ACT_LOG_SIGMOID
+    assert score_activation_code(torch.nn.Tanh())[0] == _lib.GAT_ACT_TANH
+    assert score_activation_code(torch.nn.Softmax())[0] == _lib.GAT_ACT_HEAD_SOFTMAX
+    assert score_activation_code(torch.nn.Softmax(dim=1))[0] == _lib.GAT_ACT_HEAD_SOFTMAX
+    with pytest.raises(NotImplementedError):
+        score_activation_code(torch.nn.Softmax(dim=0))
+    with pytest.raises(NotImplementedError):
+        score_activation_code(torch.nn.GELU())
+    # same parameters / state_dict as the reference's activation-test layer
+    torch.manual_seed(0)
+    a = GraphAttentionLayerActivationTest(10, 4, num_heads=2, concat=True,
+                                          activation_function=torch.nn.Tanh())
+    assert isinstance(a.attention_relu, torch.nn.Tanh)
+    assert list(a.state_dict()) == ["bias", "ws.0.weight", "ws.0.bias", "ws.1.weight",
+                                    "ws.1.bias", "attentions1.0.weight", "attentions1.0.bias",
+                                    "attentions1.1.weight", "attentions1.1.bias",
+                                    "attentions2.0.weight", "attentions2.0.bias",
+                                    "attentions2.1.weight", "attentions2.1.bias"]
