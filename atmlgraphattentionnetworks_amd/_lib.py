@@ -47,14 +47,29 @@ SIGNATURES = {
                                        _c_int, _c_int, _c_float, _c_float, _c_u64, _c_vp, _c_vp,
                                        _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_csc_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
-    "gat_csc_build": (_c_int, [_c_vp, _c_vp, _c_int, _c_ll, _c_vp, _c_vp, _c_vp, _c_vp,
+    "gat_csc_build": (_c_int, [_c_vp, _c_vp, _c_int, _c_ll, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                ctypes.c_size_t, _c_vp]),
+    "gat_bwd_table_layout": (_c_int, [_c_int, _c_int, _c_int, _c_int_p]),
+    "gat_bwd_targets": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp,
+                                 _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
+                                 _c_float, _c_float, _c_u64, _c_vp, _c_vp, _c_int, _c_int,
+                                 _c_vp]),
+    "gat_bwd_sources_parts": (_c_int, [_c_int, _c_int, _c_int, _c_int_p]),
+    "gat_bwd_sources": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int,
+                                 _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_float,
+                                 _c_float, _c_u64, _c_vp, _c_int, _c_vp, _c_int, _c_int,
+                                 _c_vp]),
     "gat_edge_backward_rows": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp,
                                         _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
-                                        _c_int, _c_int, _c_int, _c_int, _c_float, _c_float,
-                                        _c_u64, _c_vp, _c_vp, _c_vp, _c_vp]),
+                                        _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                        _c_float, _c_u64, _c_vp, _c_vp, _c_int, _c_vp]),
+    "gat_weight_grad_workspace_size": (_c_int, [_c_int, _c_int, _c_int, _c_size_p]),
+    "gat_weight_grad": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_int, _c_int, _c_vp, _c_vp,
+                                 ctypes.c_size_t, _c_vp]),
+    "gat_sum_partials_workspace_size": (_c_int, [_c_int, _c_ll, _c_size_p]),
+    "gat_sum_partials": (_c_int, [_c_vp, _c_int, _c_ll, _c_vp, _c_vp, ctypes.c_size_t, _c_vp]),
     "gat_src_backward": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
-                                  _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int,
+                                  _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int,
                                   _c_vp, _c_vp, _c_int, _c_vp]),
 }
 
@@ -122,4 +137,25 @@ def csc_workspace_size(nnz: int, num_nodes: int) -> int:
     out = ctypes.c_size_t()
     check(load().gat_csc_workspace_size(nnz, num_nodes, ctypes.byref(out)),
           "gat_csc_workspace_size")
+    return out.value
+
+
+def weight_grad_workspace_size(num_nodes: int, fin: int, hf: int) -> int:
+    out = ctypes.c_size_t()
+    check(load().gat_weight_grad_workspace_size(num_nodes, fin, hf, ctypes.byref(out)),
+          "gat_weight_grad_workspace_size")
+    return out.value
+
+
+def bwd_table_layout(heads: int, f: int, concat: bool) -> int:
+    ld = ctypes.c_int()
+    check(load().gat_bwd_table_layout(heads, f, int(concat), ctypes.byref(ld)),
+          "gat_bwd_table_layout")
+    return ld.value
+
+
+def bwd_sources_parts(num_nodes: int, heads: int, f: int) -> int:
+    out = ctypes.c_int()
+    check(load().gat_bwd_sources_parts(num_nodes, heads, f, ctypes.byref(out)),
+          "gat_bwd_sources_parts")
     return out.value

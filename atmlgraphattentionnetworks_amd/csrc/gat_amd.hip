@@ -984,22 +984,17 @@ __global__ void k_degree_keys(const int* __restrict__ rowptr, int n, unsigned* _
 // backward pass: the gradient of a source row gathers over its out-edges.
 //   csc_ptr[j]       first CSC slot of source j
 //   csc_dst[c]       target row of the edge in CSC slot c
+//   csc_eid[c]       CSR position of the edge in CSC slot c
 //   csr_to_csc[k]    CSC slot of CSR position k
 // Built by a stable radix sort of (col[k], k): within a source, edges keep
-// CSR order, so every reduction over them is deterministic.
+// CSR order, so every reduction over them is deterministic.  The target row
+// of a CSR position is found by binary search in rowptr (L2-resident) rather
+// than gathered from a per-edge array.
 // ---------------------------------------------------------------------------
-__global__ void k_edge_rows(const int* __restrict__ rowptr, int n, long long nnz,
-                            int* __restrict__ erow, unsigned* __restrict__ keys,
-                            const int* __restrict__ col, int* __restrict__ vals) {
+__global__ void k_csc_keys(long long nnz, const int* __restrict__ col,
+                           unsigned* __restrict__ keys, int* __restrict__ vals) {
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < nnz; k += stride) {
-        // the row holding position k: last i with rowptr[i] <= k
-        int lo = 0, hi = n;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (rowptr[mid] <= k) lo = mid; else hi = mid - 1;
-        }
-        erow[k] = lo;
         keys[k] = (unsigned)col[k];
         vals[k] = (int)k;
     }
@@ -1017,14 +1012,20 @@ __global__ void k_csc_ptr(const unsigned* __restrict__ sorted_keys, long long nn
     csc_ptr[j] = (int)lo;
 }
 
-__global__ void k_csc_fill(const int* __restrict__ sorted_vals, const int* __restrict__ erow,
-                           long long nnz, int* __restrict__ csc_dst,
+__global__ void k_csc_fill(const int* __restrict__ sorted_vals, const int* __restrict__ rowptr,
+                           int n, long long nnz, int* __restrict__ csc_dst,
                            int* __restrict__ csr_to_csc) {
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x; c < nnz; c += stride) {
         const int k = sorted_vals[c];
-        csr_to_csc[k] = (int)c;
-        csc_dst[c] = erow[k];
+        // the row holding CSR position k: last i with rowptr[i] <= k
+        int lo = 0, hi = n - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (rowptr[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        csc_dst[c] = lo;
+        if (csr_to_csc != nullptr) csr_to_csc[k] = (int)c;
     }
 }
 
@@ -1038,8 +1039,8 @@ __global__ void k_csc_fill(const int* __restrict__ sorted_vals, const int* __res
 //   de        = alpha * (dA - delta_h)              softmax backward
 //   dz        = de * (z > 0 ? 1 : slope)            LeakyReLU backward
 //   ds_dst[i] = sum_edges dz
-// and stores A and dz per (edge, head) at the edge's CSC slot, so pass 2
-// reads them contiguously.
+// and stores (A, dz) per (edge, head) — interleaved, one 8H-byte record per
+// edge — at the edge's CSC slot, so pass 2 reads them contiguously.
 // Algorithmic bytes per edge: 4 (col) + 4 (csr_to_csc) + 4H (s_src) + 4HF (Wh
 // row) + 8H (A, dz); per row: 4HF (g) + 4HF (y) + 8H (s_dst, lse) + 4H.
 // ---------------------------------------------------------------------------
@@ -1051,7 +1052,7 @@ __global__ __launch_bounds__(64) void k_edge_bwd_rows(
     const float* __restrict__ s_dst, const float* __restrict__ lse,
     const float* __restrict__ y_heads, const float* __restrict__ g, int H, int F, int HF,
     int concat, int act, float slope, DropArgs drop, float* __restrict__ ds_dst,
-    float* __restrict__ alpha_out, float* __restrict__ dz_out) {
+    float2* __restrict__ az_out) {
     constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;
     constexpr int R = C * HP / kWave;
     __shared__ float dy_s[GAT_MAX_HF];
@@ -1115,9 +1116,7 @@ __global__ __launch_bounds__(64) void k_edge_bwd_rows(
             }
             if (valid) {
                 dsd += dz;
-                const size_t o = (size_t)slot_s[k] * H + hs;
-                alpha_out[o] = a * dm;
-                dz_out[o] = dz;
+                az_out[(size_t)slot_s[k] * H + hs] = make_float2(a * dm, dz);
             }
         }
         __syncthreads();
@@ -1128,16 +1127,369 @@ __global__ __launch_bounds__(64) void k_edge_bwd_rows(
 }
 
 // ---------------------------------------------------------------------------
+// Backward, pass 1, lane-group variant (LeakyReLU, F/4 a power of two): the
+// k_edge_grp layout — G lanes per target row, each lane one float4 of one
+// head — so each in-edge costs one coalesced Wh-row gather, the source score
+// is recomputed from it (fused, as in the forward) and the two per-head dot
+// products (s_src and dA = dy . Wh[j]) are DPP sums over the head's lanes.
+// No LDS, no barriers; col and csr_to_csc loads software-pipelined.
+// Same results as k_edge_bwd_rows up to fp32 rounding.
+// ---------------------------------------------------------------------------
+template <int G, int U>
+__global__ __launch_bounds__(256) void k_edge_bwd_grp(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
+    int row_begin, int row_end, const int* __restrict__ csr_to_csc,
+    const float* __restrict__ Wh, int ld_wh, const float* __restrict__ a_src,
+    const float* __restrict__ c_src, const float* __restrict__ s_dst,
+    const float* __restrict__ lse, const float* __restrict__ y_heads,
+    const float* __restrict__ g, int H, int F, int HF, int concat, float slope, DropArgs drop,
+    float* __restrict__ ds_dst, float2* __restrict__ az_out) {
+    constexpr int CL = (U + G - 1) / G;
+    const int lane = threadIdx.x & 63;
+    const int c = lane & (G - 1);
+    const int gbase = lane & ~(G - 1);
+    const int pos = row_begin + (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    if (pos >= row_end) return;
+    const int r = order != nullptr ? order[pos] : pos;
+    const bool c_ok = 4 * c < HF;
+    const int coff = c_ok ? 4 * c : 0;
+    const int h = coff / F;
+    const int hl = F / 4;  // lanes per head
+    const bool leader = c_ok && (coff % F) == 0;
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 a4 = c_ok ? *reinterpret_cast<const f32x4*>(a_src + coff) : zero4;
+    const float c1 = c_src[h];
+    f32x4 dy = zero4, yv = zero4;
+    if (c_ok) {
+        if (concat) {
+            dy = *reinterpret_cast<const f32x4*>(g + (size_t)r * HF + coff);
+        } else {
+            dy = *reinterpret_cast<const f32x4*>(g + (size_t)r * F + (coff % F));
+            dy *= 1.f / (float)H;
+        }
+        yv = *reinterpret_cast<const f32x4*>(y_heads + (size_t)r * HF + coff);
+    }
+    auto hsum = [&](float v) {
+        if (hl <= 16) return group_sum16(v, hl);
+        for (int off = 1; off < hl; off <<= 1) v += __shfl_xor(v, off);
+        return v;
+    };
+    const float dl = hsum(dy.x * yv.x + dy.y * yv.y + dy.z * yv.z + dy.w * yv.w);
+    const float sd = s_dst[(size_t)r * H + h] + c1;
+    const float ls2 = lse[(size_t)r * H + h] * kLog2e;
+    const int e0 = rowptr[r], e1 = rowptr[r + 1];
+    float dsd = 0.f;
+    int cv[CL], sv[CL];
+#pragma unroll
+    for (int t = 0; t < CL; ++t) {
+        const int kk = min(e0 + c + t * G, e1 - 1);
+        cv[t] = col[kk];
+        sv[t] = csr_to_csc[kk];
+    }
+    for (int k = e0; k < e1; k += U) {
+        const int nk = min(U, e1 - k);
+        int cn[CL], sn[CL];
+#pragma unroll
+        for (int t = 0; t < CL; ++t) {
+            const int kk = min(k + U + c + t * G, e1 - 1);
+            cn[t] = col[kk];
+            sn[t] = csr_to_csc[kk];
+        }
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = __shfl(cv[u / G], gbase + (u % G));
+            v[u] = *reinterpret_cast<const f32x4*>(Wh + (size_t)j * ld_wh + coff);
+        }
+        float ss[U], da[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ss[u] = v[u].x * a4.x + v[u].y * a4.y + v[u].z * a4.z + v[u].w * a4.w;
+            da[u] = v[u].x * dy.x + v[u].y * dy.y + v[u].z * dy.z + v[u].w * dy.w;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ss[u] = hsum(ss[u]);
+            da[u] = hsum(da[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int slot = __shfl(sv[u / G], gbase + (u % G));
+            const float z = sd + ss[u];
+            const float a = __builtin_amdgcn_exp2f(fmaxf(z, z * slope) * kLog2e - ls2);
+            const float dm = drop.thresh != 0u ? drop_factor(drop, k + u, h, H) : 1.f;
+            const float de = a * (dm * da[u] - dl);
+            const float dz = z > 0.f ? de : de * slope;
+            if (u < nk) {
+                dsd += dz;
+                if (leader) az_out[(size_t)slot * H + h] = make_float2(a * dm, dz);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < CL; ++t) {
+            cv[t] = cn[t];
+            sv[t] = sn[t];
+        }
+    }
+    if (leader) ds_dst[(size_t)r * H + h] = dsd;
+}
+
+// ---------------------------------------------------------------------------
+// Recompute backward (LeakyReLU, F/4 a power of two): no per-edge state.
+//
+// Pass 1, per TARGET row i (k_edge_grp layout): delta_h = dy_h . y_h, then over
+// the in-edges the same recomputation as k_edge_bwd_grp, accumulating only
+// ds_dst[i].  Writes one row of the target table
+//   T[i] = [ g_i (ldg, 0-padded to 4) | per head (s_dst, lse, delta, 0) ]
+// so pass 2 gathers everything it needs about a target with two float4 loads
+// per lane.  Per edge: 4 (col) + 4HF (Wh row) bytes, as the forward.
+// ---------------------------------------------------------------------------
+template <int G, int U>
+__global__ __launch_bounds__(256) void k_bwd_targets(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
+    int row_begin, int row_end, const float* __restrict__ Wh, int ld_wh,
+    const float* __restrict__ a_src, const float* __restrict__ c_src,
+    const float* __restrict__ s_dst, const float* __restrict__ lse,
+    const float* __restrict__ y_heads, const float* __restrict__ g, int H, int F, int HF,
+    int concat, float slope, DropArgs drop, float* __restrict__ ds_dst,
+    float* __restrict__ T, int ld_t) {
+    constexpr int CL = (U + G - 1) / G;
+    const int lane = threadIdx.x & 63;
+    const int c = lane & (G - 1);
+    const int gbase = lane & ~(G - 1);
+    const int pos = row_begin + (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    if (pos >= row_end) return;
+    const int r = order != nullptr ? order[pos] : pos;
+    const bool c_ok = 4 * c < HF;
+    const int coff = c_ok ? 4 * c : 0;
+    const int h = coff / F;
+    const int hl = F / 4;
+    const bool leader = c_ok && (coff % F) == 0;
+    const int ldg = concat ? HF : F;
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 a4 = c_ok ? *reinterpret_cast<const f32x4*>(a_src + coff) : zero4;
+    const float c1 = c_src[h];
+    f32x4 g4 = zero4, yv = zero4;
+    const bool g_ok = c_ok && (concat || coff < F);
+    if (c_ok) {
+        g4 = *reinterpret_cast<const f32x4*>(g + (size_t)r * ldg + (concat ? coff : coff % F));
+        yv = *reinterpret_cast<const f32x4*>(y_heads + (size_t)r * HF + coff);
+    }
+    const f32x4 dy = concat ? g4 : g4 * (1.f / (float)H);
+    auto hsum = [&](float v) {
+        if (hl <= 16) return group_sum16(v, hl);
+        for (int off = 1; off < hl; off <<= 1) v += __shfl_xor(v, off);
+        return v;
+    };
+    const float dl = hsum(dy.x * yv.x + dy.y * yv.y + dy.z * yv.z + dy.w * yv.w);
+    const float sdv = s_dst[(size_t)r * H + h];
+    const float lsv = lse[(size_t)r * H + h];
+    const float sd = sdv + c1;
+    const float ls2 = lsv * kLog2e;
+    const int e0 = rowptr[r], e1 = rowptr[r + 1];
+    float dsd = 0.f;
+    int cv[CL];
+#pragma unroll
+    for (int t = 0; t < CL; ++t) cv[t] = col[min(e0 + c + t * G, e1 - 1)];
+    for (int k = e0; k < e1; k += U) {
+        const int nk = min(U, e1 - k);
+        int cn[CL];
+#pragma unroll
+        for (int t = 0; t < CL; ++t) cn[t] = col[min(k + U + c + t * G, e1 - 1)];
+        f32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = __shfl(cv[u / G], gbase + (u % G));
+            v[u] = *reinterpret_cast<const f32x4*>(Wh + (size_t)j * ld_wh + coff);
+        }
+        float ss[U], da[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ss[u] = hsum(v[u].x * a4.x + v[u].y * a4.y + v[u].z * a4.z + v[u].w * a4.w);
+            da[u] = hsum(v[u].x * dy.x + v[u].y * dy.y + v[u].z * dy.z + v[u].w * dy.w);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float z = sd + ss[u];
+            const float a = __builtin_amdgcn_exp2f(fmaxf(z, z * slope) * kLog2e - ls2);
+            const float dm = drop.thresh != 0u ? drop_factor(drop, k + u, h, H) : 1.f;
+            const float de = a * (dm * da[u] - dl);
+            const float dz = z > 0.f ? de : de * slope;
+            dsd += u < nk ? dz : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < CL; ++t) cv[t] = cn[t];
+    }
+    float* tr = T + (size_t)r * ld_t;
+    if (g_ok) *reinterpret_cast<f32x4*>(tr + coff) = g4;
+    if (leader) {
+        ds_dst[(size_t)r * H + h] = dsd;
+        *reinterpret_cast<f32x4*>(tr + round_up4(ldg) + 4 * h) = f32x4{sdv, lsv, dl, 0.f};
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 2, per SOURCE row j (lane-group layout over the CSC): lane owns one
+// float4 of Wh[j] (one head).  Per out-edge j -> i (slot e, CSR position
+// k = csc_eid[e]): gather T[i] (the lane's g float4 + its head's
+// (s_dst, lse, delta)), recompute
+//   z = s_dst[i] + s_src[j], A = drop * exp(LReLU(z) - lse[i]),
+//   dA = drop * (dy_i . Wh[j]) (DPP head sum), dz = A_undropped (dA - delta) LReLU'(z)
+// and accumulate dWh[j] += A dy_i, ds_src[j] += dz.  Rows are strided over a
+// fixed grid; each lane keeps its rows' contributions to da1/da2/dc1/dc2/db/
+// dbias in registers, the wave's groups are combined by xor-shuffles and the
+// wave writes one partial row [da1 | da2 | dc1 | dc2 | db | dbias] (summed by
+// gat_sum_partials; deterministic).
+// Per edge: 4 (csc_dst) + 4 (csc_eid, with dropout) + 4 ldg + 16 H bytes.
+// ---------------------------------------------------------------------------
+template <int G, int U>
+__global__ __launch_bounds__(256) void k_bwd_sources(
+    const int* __restrict__ csc_ptr, const int* __restrict__ csc_dst,
+    const int* __restrict__ csc_eid, int n, const float* __restrict__ Wh, int ld_wh,
+    const float* __restrict__ T, int ld_t, const float* __restrict__ ds_dst,
+    const float* __restrict__ a_src, const float* __restrict__ c_src,
+    const float* __restrict__ a_dst, int H, int F, int HF, int concat, float slope,
+    DropArgs drop, float* __restrict__ dwh, int ld_dwh, float* __restrict__ part) {
+    constexpr int CL = (U + G - 1) / G;
+    const int lane = threadIdx.x & 63;
+    const int c = lane & (G - 1);
+    const int gbase = lane & ~(G - 1);
+    const int groups = (gridDim.x * blockDim.x) / G;
+    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    const bool c_ok = 4 * c < HF;
+    const int coff = c_ok ? 4 * c : 0;
+    const int h = coff / F;
+    const int hl = F / 4;
+    const bool leader = c_ok && (coff % F) == 0;
+    const int ldg = concat ? HF : F;
+    const int toff = round_up4(ldg) + 4 * h;
+    const int goff = concat ? coff : coff % F;
+    const bool g_ok = c_ok && (concat || coff < F);
+    const float gs = concat ? 1.f : 1.f / (float)H;
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 a1 = c_ok ? *reinterpret_cast<const f32x4*>(a_src + coff) : zero4;
+    const f32x4 a2 = c_ok ? *reinterpret_cast<const f32x4*>(a_dst + coff) : zero4;
+    const float c1 = c_src[h];
+    auto hsum = [&](float v) {
+        if (hl <= 16) return group_sum16(v, hl);
+        for (int off = 1; off < hl; off <<= 1) v += __shfl_xor(v, off);
+        return v;
+    };
+    f32x4 pa1 = zero4, pa2 = zero4, pdb = zero4, pbias = zero4;
+    float pc1 = 0.f, pc2 = 0.f;
+    const bool use_drop = drop.thresh != 0u;
+    for (int j = gid; j < n; j += groups) {
+        const f32x4 w4 = c_ok ? *reinterpret_cast<const f32x4*>(Wh + (size_t)j * ld_wh + coff)
+                              : zero4;
+        const float ssrc = hsum(w4.x * a1.x + w4.y * a1.y + w4.z * a1.z + w4.w * a1.w) + c1;
+        const int b0 = csc_ptr[j], b1 = csc_ptr[j + 1];
+        f32x4 acc = zero4;
+        float dss = 0.f;
+        int iv[CL], kv[CL];
+#pragma unroll
+        for (int t = 0; t < CL; ++t) {
+            const int bb = max(min(b0 + c + t * G, b1 - 1), 0);
+            iv[t] = csc_dst[bb];
+            kv[t] = use_drop ? csc_eid[bb] : 0;
+        }
+        for (int b = b0; b < b1; b += U) {
+            const int nb = min(U, b1 - b);
+            int in_[CL], kn[CL];
+#pragma unroll
+            for (int t = 0; t < CL; ++t) {
+                const int bb = min(b + U + c + t * G, b1 - 1);
+                in_[t] = csc_dst[bb];
+                kn[t] = use_drop ? csc_eid[bb] : 0;
+            }
+            f32x4 gv[U], tv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = __shfl(iv[u / G], gbase + (u % G));
+                const float* tr = T + (size_t)i * ld_t;
+                gv[u] = g_ok || !concat ? *reinterpret_cast<const f32x4*>(tr + goff) : zero4;
+                tv[u] = *reinterpret_cast<const f32x4*>(tr + toff);
+            }
+            float da[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                da[u] = hsum(gv[u].x * w4.x + gv[u].y * w4.y + gv[u].z * w4.z + gv[u].w * w4.w);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int kpos = __shfl(kv[u / G], gbase + (u % G));
+                const float z = tv[u].x + ssrc;
+                const float a = expf(fmaxf(z, z * slope) - tv[u].y);
+                const float dm = use_drop ? drop_factor(drop, kpos, h, H) : 1.f;
+                const float de = a * (dm * da[u] * gs - tv[u].z);
+                const float dz = z > 0.f ? de : de * slope;
+                const float w = u < nb ? a * dm : 0.f;
+                acc += w * gv[u];
+                dss += u < nb ? dz : 0.f;
+            }
+#pragma unroll
+            for (int t = 0; t < CL; ++t) {
+                iv[t] = in_[t];
+                kv[t] = kn[t];
+            }
+        }
+        const float dsd = ds_dst[(size_t)j * H + h];
+        const f32x4 d = acc * gs + dss * a1 + dsd * a2;
+        if (c_ok) *reinterpret_cast<f32x4*>(dwh + (size_t)j * ld_dwh + coff) = d;
+        pa1 += dss * w4;
+        pa2 += dsd * w4;
+        pdb += c_ok ? d : zero4;
+        if (g_ok) pbias += *reinterpret_cast<const f32x4*>(T + (size_t)j * ld_t + goff);
+        if (leader) {
+            pc1 += dss;
+            pc2 += dsd;
+        }
+    }
+    // combine the wave's 64/G groups (same columns in every group)
+#pragma unroll
+    for (int off = G; off < kWave; off <<= 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            pa1[q] += __shfl_xor(pa1[q], off);
+            pa2[q] += __shfl_xor(pa2[q], off);
+            pdb[q] += __shfl_xor(pdb[q], off);
+            pbias[q] += __shfl_xor(pbias[q], off);
+        }
+        pc1 += __shfl_xor(pc1, off);
+        pc2 += __shfl_xor(pc2, off);
+    }
+    if (lane >= G) return;
+    const int wave = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave);
+    float* pw = part + (size_t)wave * (3 * HF + 2 * H + ldg);
+    if (c_ok) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            pw[coff + q] = pa1[q];
+            pw[HF + coff + q] = pa2[q];
+            pw[2 * HF + 2 * H + coff + q] = pdb[q];
+        }
+    }
+    if (g_ok) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pw[3 * HF + 2 * H + goff + q] = pbias[q];
+    }
+    if (leader) {
+        pw[2 * HF + h] = pc1;
+        pw[2 * HF + H + h] = pc2;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Backward, pass 2: one wave per SOURCE row j (CSC, grid-stride), lanes over
 // the HF columns (CQ per lane).  Over j's out-edges (target i, slot c):
 //   dWh[j]    = sum_c A[c,h] * dy[i]_h            (message backward)
 //   ds_src[j] = sum_c dz[c]
 // then the score terms s_src = Wh.a1 + c1, s_dst = Wh.a2 + c2 fold in:
 //   dWh_total[j] = dWh[j] + ds_src[j,h] a1_h + ds_dst[j,h] a2_h
-// and each wave accumulates its rows' contributions to da1/da2 (ds * Wh) and
-// dc1/dc2 (ds) in registers, written once as per-wave partials
-// part[w] = [da1 (HF) | da2 (HF) | dc1 (H) | dc2 (H)] — summed by the caller;
-// no float atomics, so the result is run-to-run deterministic.
+// and each wave accumulates its rows' contributions to da1/da2 (ds * Wh),
+// dc1/dc2 (ds), db (= sum of dWh_total rows, the projection bias gradient)
+// and dbias (= sum of grad_out rows) in registers, written once as per-wave
+// partials part[w] = [da1 (HF) | da2 (HF) | dc1 (H) | dc2 (H) | db (HF) |
+// dbias (ldg)] — summed by the caller; no float atomics, so the result is
+// run-to-run deterministic.
 // Algorithmic bytes per edge: 4 (csc_dst) + 4HF (g row, concat; 4F mean)
 // + 8H (A, dz); per row: 4HF (Wh) + 4HF (dWh) + 8H.
 // ---------------------------------------------------------------------------
@@ -1145,8 +1497,7 @@ template <int CQ, int HP>
 __global__ __launch_bounds__(64) void k_src_bwd(
     const int* __restrict__ csc_ptr, const int* __restrict__ csc_dst, int n,
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ g,
-    const float* __restrict__ alpha, const float* __restrict__ dz,
-    const float* __restrict__ ds_dst, const float* __restrict__ a1, const float* __restrict__ a2,
+    const float2* __restrict__ az, const float* __restrict__ ds_dst, const float* __restrict__ a1, const float* __restrict__ a2,
     int H, int F, int HF, int concat, float* __restrict__ dwh, int ld_dwh,
     float* __restrict__ ds_src, float* __restrict__ part) {
     __shared__ float dss_s[HP];
@@ -1156,7 +1507,7 @@ __global__ __launch_bounds__(64) void k_src_bwd(
     const float inv_h = 1.f / (float)H;
     int cc[CQ], hq[CQ], gq[CQ];
     bool okq[CQ];
-    float a1v[CQ], a2v[CQ], pa1[CQ], pa2[CQ];
+    float a1v[CQ], a2v[CQ], pa1[CQ], pa2[CQ], pdb[CQ], pbias[CQ];
 #pragma unroll
     for (int q = 0; q < CQ; ++q) {
         const int c = lane + kWave * q;
@@ -1168,6 +1519,8 @@ __global__ __launch_bounds__(64) void k_src_bwd(
         a2v[q] = okq[q] ? a2[cc[q]] : 0.f;
         pa1[q] = 0.f;
         pa2[q] = 0.f;
+        pdb[q] = 0.f;
+        pbias[q] = 0.f;
     }
     const int ldg = concat ? HF : F;
     const float gs = concat ? 1.f : inv_h;
@@ -1195,9 +1548,9 @@ __global__ __launch_bounds__(64) void k_src_bwd(
 #pragma unroll
                 for (int q = 0; q < CQ; ++q) {
                     gv[u][q] = g[(size_t)iu[u] * ldg + gq[q]];
-                    av[u][q] = alpha[(size_t)su[u] * H + hq[q]];
+                    av[u][q] = az[(size_t)su[u] * H + hq[q]].x;
                 }
-                zv[u] = h_ok ? dz[(size_t)su[u] * H + lane] : 0.f;
+                zv[u] = h_ok ? az[(size_t)su[u] * H + lane].y : 0.f;
             }
 #pragma unroll
             for (int u = 0; u < UE; ++u) {
@@ -1217,10 +1570,13 @@ __global__ __launch_bounds__(64) void k_src_bwd(
                 const float hsrc = dss_s[hq[q]];
                 const float hdst = ds_dst[(size_t)j * H + hq[q]];
                 const float whv = Wh[(size_t)j * ld_wh + cc[q]];
-                dwh[(size_t)j * ld_dwh + cc[q]] = fmaf(hdst, a2v[q], fmaf(hsrc, a1v[q], acc[q] * gs));
+                const float d = fmaf(hdst, a2v[q], fmaf(hsrc, a1v[q], acc[q] * gs));
+                dwh[(size_t)j * ld_dwh + cc[q]] = d;
                 pa1[q] = fmaf(hsrc, whv, pa1[q]);
                 pa2[q] = fmaf(hdst, whv, pa2[q]);
+                pdb[q] += d;
             }
+            if (cc[q] < ldg && okq[q]) pbias[q] += g[(size_t)j * ldg + cc[q]];
         }
         if (h_ok) {
             pc1 += dss;
@@ -1228,18 +1584,129 @@ __global__ __launch_bounds__(64) void k_src_bwd(
         }
         __syncthreads();
     }
-    float* pw = part + (size_t)w * (2 * HF + 2 * H);
+    float* pw = part + (size_t)w * (3 * HF + 2 * H + ldg);
 #pragma unroll
     for (int q = 0; q < CQ; ++q) {
         if (okq[q]) {
             pw[cc[q]] = pa1[q];
             pw[HF + cc[q]] = pa2[q];
+            pw[2 * HF + 2 * H + cc[q]] = pdb[q];
+            if (cc[q] < ldg) pw[3 * HF + 2 * H + cc[q]] = pbias[q];
         }
     }
     if (h_ok) {
         pw[2 * HF + lane] = pc1;
         pw[2 * HF + H + lane] = pc2;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient of the projection: dW[HF, Fin] = dWh^T x, a contraction
+// over all N rows (K = N), which library GEMM heuristics handle poorly (one
+// 165 us hipBLASLt call at PPI shape).  Split-K on fp32 MFMA 16x16x4: block
+// (fin tile of 64, row chunk s, hf tile of 64); wave w owns hf rows
+// [16w, 16w+16) of the tile and all four 16-wide fin sub-tiles, so per 4 rows
+// a lane issues 1 dWh + 4 x loads and 4 MFMAs.  Operands come straight from
+// global memory (each row is read by one block: no reuse for LDS to exploit).
+// part[s] = the chunk's [HF, Fin] partial; k_wgrad_reduce sums the chunks in
+// a fixed order (deterministic).
+// Algorithmic bytes: 4 N (HF + Fin) reads + 4 S HF Fin partials.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dwh, int ld_dwh,
+                                               const float* __restrict__ x, int n, int fin,
+                                               int hf, int rows_per_chunk,
+                                               float* __restrict__ part) {
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int j0 = blockIdx.x * 64;
+    const int s = blockIdx.y;
+    const int i0 = blockIdx.z * 64 + wv * 16;
+    const int r0 = s * rows_per_chunk;
+    const int r1 = min(n, r0 + rows_per_chunk);
+    const int kk = lane >> 4, ii = lane & 15;
+    const int icol = i0 + ii;
+    const bool i_ok = icol < hf;
+    const float amask = i_ok ? 1.f : 0.f;
+    const int ic = i_ok ? icol : 0;
+    int jc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) jc[t] = min(j0 + 16 * t + ii, fin - 1);
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int UR = 4;  // 4-row MFMA steps in flight
+    for (int r = r0; r < r1; r += 4 * UR) {
+        float av[UR], bv[UR][4];
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int row = r + 4 * u + kk;
+            const bool ok = row < r1;
+            const int rr = ok ? row : r1 - 1;
+            av[u] = dwh[(size_t)rr * ld_dwh + ic] * (ok ? amask : 0.f);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) bv[u][t] = x[(size_t)rr * fin + jc[t]];
+        }
+#pragma unroll
+        for (int u = 0; u < UR; ++u)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u][t], acc[t], 0, 0, 0);
+    }
+    // C[i][j]: j = lane & 15, i = 4 * (lane >> 4) + q
+    float* ps = part + (size_t)s * hf * fin;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int j = j0 + 16 * t + ii;
+        if (j >= fin) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int i = i0 + 4 * kk + q;
+            if (i < hf) ps[(size_t)i * fin + j] = acc[t][q];
+        }
+    }
+}
+
+// out[b * width + e] = sum_c part[c * width + e] over rows c of row block
+// b = blockIdx.y ([b * rows_per_block, ...) ∩ [0, rows)): 16 columns x 16 row
+// groups per block, 4 independent loads in flight per thread, then a fixed
+// order combine in LDS (deterministic).  Sums the per-chunk / per-wave
+// partials of k_wgrad and k_src_bwd.
+__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ part, int rows,
+                                                long long width, float* __restrict__ out,
+                                                int rows_per_block) {
+    __shared__ float red[16][17];
+    const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const long long e = blockIdx.x * 16LL + col;
+    const long long ec = e < width ? e : width - 1;
+    const int rb0 = blockIdx.y * rows_per_block;
+    part += (size_t)rb0 * width;
+    out += (size_t)blockIdx.y * width;
+    rows = min(rows - rb0, rows_per_block);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int c = grp;
+    for (; c + 48 < rows; c += 64) {
+        s0 += part[(size_t)c * width + ec];
+        s1 += part[(size_t)(c + 16) * width + ec];
+        s2 += part[(size_t)(c + 32) * width + ec];
+        s3 += part[(size_t)(c + 48) * width + ec];
+    }
+    for (; c < rows; c += 16) s0 += part[(size_t)c * width + ec];
+    red[grp][col] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (grp == 0 && e < width) {
+        float t = 0.f;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) t += red[g][col];
+        out[e] = t;
+    }
+}
+
+int wgrad_chunks(int n, int fin, int hf) {
+    const int ftiles = (fin + 63) / 64, htiles = (hf + 63) / 64;
+    int by_rows = (n + 255) / 256;
+    int by_fill = (2048 + ftiles * htiles - 1) / (ftiles * htiles);
+    int c = by_rows < by_fill ? by_rows : by_fill;
+    return c < 1 ? 1 : c;
 }
 
 constexpr size_t kAlign = 256;
@@ -1607,13 +2074,13 @@ int gat_csc_workspace_size(long long nnz, int num_nodes, size_t* bytes) {
     if (nnz < 0 || num_nodes < 0 || bytes == nullptr) return GAT_EINVAL;
     if (nnz > 0x7fffffffLL) return GAT_EUNSUPPORTED;
     const size_t eb = align_up((size_t)(nnz > 0 ? nnz : 1) * 4);
-    *bytes = 5 * eb + align_up(radix_tmp_bytes(nnz, num_nodes > 0 ? num_nodes : 1));
+    *bytes = 4 * eb + align_up(radix_tmp_bytes(nnz, num_nodes > 0 ? num_nodes : 1));
     return GAT_OK;
 }
 
 int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nnz, int* csc_ptr,
-                  int* csc_dst, int* csr_to_csc, void* workspace, size_t workspace_bytes,
-                  void* stream) {
+                  int* csc_dst, int* csc_eid, int* csr_to_csc, void* workspace,
+                  size_t workspace_bytes, void* stream) {
     if (num_nodes < 0 || nnz < 0) return GAT_EINVAL;
     size_t need = 0;
     int rc = gat_csc_workspace_size(nnz, num_nodes, &need);
@@ -1624,32 +2091,138 @@ int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nn
     if (nnz == 0) return status_of(hipMemsetAsync(csc_ptr, 0, sizeof(int) * (num_nodes + 1), st));
     const size_t eb = align_up((size_t)nnz * 4);
     char* ws = (char*)workspace;
-    int* erow = (int*)ws;
-    unsigned* keys_in = (unsigned*)(ws + eb);
-    int* vals_in = (int*)(ws + 2 * eb);
-    unsigned* keys_out = (unsigned*)(ws + 3 * eb);
-    int* vals_out = (int*)(ws + 4 * eb);
-    void* tmp = ws + 5 * eb;
-    hipLaunchKernelGGL(k_edge_rows, dim3(grid_for(nnz, 256)), dim3(256), 0, st, rowptr,
-                       num_nodes, nnz, erow, keys_in, col, vals_in);
-    size_t tmp_bytes = need - 5 * eb;
+    unsigned* keys_in = (unsigned*)ws;
+    int* vals_in = (int*)(ws + eb);
+    unsigned* keys_out = (unsigned*)(ws + 2 * eb);
+    int* vals_out = csc_eid != nullptr ? csc_eid : (int*)(ws + 3 * eb);
+    void* tmp = ws + 4 * eb;
+    hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(nnz, 256)), dim3(256), 0, st, nnz, col, keys_in,
+                       vals_in);
+    size_t tmp_bytes = need - 4 * eb;
     hipError_t e = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out,
                                              (size_t)nnz, 0u, key_bits(num_nodes), st);
     if (e != hipSuccess) return status_of(e);
     hipLaunchKernelGGL(k_csc_ptr, dim3((num_nodes + 1 + 255) / 256), dim3(256), 0, st, keys_out,
                        nnz, num_nodes, csc_ptr);
-    hipLaunchKernelGGL(k_csc_fill, dim3(grid_for(nnz, 256)), dim3(256), 0, st, vals_out, erow,
-                       nnz, csc_dst, csr_to_csc);
+    hipLaunchKernelGGL(k_csc_fill, dim3(grid_for(nnz, 256)), dim3(256), 0, st, vals_out, rowptr,
+                       num_nodes, nnz, csc_dst, csr_to_csc);
+    return status_of(hipGetLastError());
+}
+
+int gat_bwd_table_layout(int heads, int f, int concat, int* ld_t) {
+    if (heads <= 0 || f <= 0 || ld_t == nullptr) return GAT_EINVAL;
+    *ld_t = round_up4(concat ? heads * f : f) + 4 * heads;
+    return GAT_OK;
+}
+
+static bool bwd_recompute_ok(int heads, int f, float slope, const float* wh, int ld_wh) {
+    // GAT_BWD_KERNEL=stored|generic (A/B knob): force the stored-coefficient path
+    if (const char* v = std::getenv("GAT_BWD_KERNEL"))
+        if (std::strcmp(v, "stored") == 0 || std::strcmp(v, "generic") == 0) return false;
+    const int hl = f / 4;
+    return heads * f <= GAT_MAX_HF && heads <= GAT_MAX_HEADS && f % 4 == 0 &&
+           next_pow2(hl) == hl && slope >= 0.f && slope <= 1.f && (ld_wh & 3) == 0 &&
+           (reinterpret_cast<uintptr_t>(wh) & 15) == 0;
+}
+
+int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int row_begin,
+                    int row_end, const float* wh, int ld_wh, const float* a_src,
+                    const float* c_src, const float* s_dst, const float* lse,
+                    const float* y_heads, const float* grad_out, int heads, int f, int concat,
+                    float negative_slope, float dropout_p, unsigned long long seed,
+                    float* ds_dst, float* table, int ld_t, int edges_per_row_hint,
+                    void* stream) {
+    if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
+    if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
+    int need_ld = 0;
+    gat_bwd_table_layout(heads, f, concat, &need_ld);
+    if (ld_t < need_ld || (ld_t & 3)) return GAT_EINVAL;
+    if (!bwd_recompute_ok(heads, f, negative_slope, wh, ld_wh)) return GAT_EUNSUPPORTED;
+    const int rows = row_end - row_begin;
+    if (rows == 0) return GAT_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const DropArgs drop = make_drop(dropout_p, seed);
+    const int hf = heads * f;
+    const int g = next_pow2(hf / 4);
+    const int u = edges_per_row_hint > 0 && edges_per_row_hint <= 12 ? 4 : 8;
+    const long long threads = (long long)rows * g;
+    const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+#define GAT_BT(G, UU)                                                                         \
+    hipLaunchKernelGGL((k_bwd_targets<G, UU>), grid, block, 0, st, rowptr, col, row_order,    \
+                       row_begin, row_end, wh, ld_wh, a_src, c_src, s_dst, lse, y_heads,      \
+                       grad_out, heads, f, hf, concat, negative_slope, drop, ds_dst, table,   \
+                       ld_t)
+#define GAT_BT_U(G)                      \
+    case G:                              \
+        if (u == 4) { GAT_BT(G, 4); }    \
+        else { GAT_BT(G, 8); }           \
+        break;
+    switch (g) {
+        GAT_BT_U(1) GAT_BT_U(2) GAT_BT_U(4) GAT_BT_U(8) GAT_BT_U(16) GAT_BT_U(32) GAT_BT_U(64)
+        default: return GAT_EUNSUPPORTED;
+    }
+#undef GAT_BT_U
+#undef GAT_BT
+    return status_of(hipGetLastError());
+}
+
+int gat_bwd_sources_parts(int num_nodes, int heads, int f, int* num_parts) {
+    if (num_nodes < 0 || heads <= 0 || f <= 0 || num_parts == nullptr) return GAT_EINVAL;
+    const int g = next_pow2((heads * f + 3) / 4);
+    const long long waves = ((long long)num_nodes * g + kWave - 1) / kWave;
+    long long cap = 65536;  // GAT_BWD_WAVES overrides (A/B knob)
+    if (const char* v = std::getenv("GAT_BWD_WAVES")) cap = std::atoll(v) > 0 ? std::atoll(v) : cap;
+    long long w = waves < cap ? waves : cap;
+    w = (w + 3) / 4 * 4;  // whole 256-thread blocks
+    *num_parts = (int)(w < 4 ? 4 : w);
+    return GAT_OK;
+}
+
+int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, int num_nodes,
+                    const float* wh, int ld_wh, const float* table, int ld_t,
+                    const float* ds_dst, const float* a_src, const float* c_src,
+                    const float* a_dst, int heads, int f, int concat, float negative_slope,
+                    float dropout_p, unsigned long long seed, float* dwh, int ld_dwh,
+                    float* partials, int num_parts, int edges_per_row_hint, void* stream) {
+    if (heads <= 0 || f <= 0 || num_nodes < 0 || num_parts <= 0 || (num_parts & 3))
+        return GAT_EINVAL;
+    if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
+    const int hf = heads * f;
+    if (ld_dwh < hf || (ld_dwh & 3)) return GAT_EINVAL;
+    if (!bwd_recompute_ok(heads, f, negative_slope, wh, ld_wh)) return GAT_EUNSUPPORTED;
+    if (dropout_p > 0.f && csc_eid == nullptr) return GAT_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const DropArgs drop = make_drop(dropout_p, seed);
+    const int g = next_pow2(hf / 4);
+    int u = edges_per_row_hint > 0 && edges_per_row_hint <= 12 ? 4 : 8;
+    if (const char* v = std::getenv("GAT_BWD_U")) u = std::atoi(v) == 4 ? 4 : 8;  // A/B knob
+    const dim3 grid(num_parts / 4), block(256);
+#define GAT_BS(G, UU)                                                                         \
+    hipLaunchKernelGGL((k_bwd_sources<G, UU>), grid, block, 0, st, csc_ptr, csc_dst, csc_eid,  \
+                       num_nodes, wh, ld_wh, table, ld_t, ds_dst, a_src, c_src, a_dst, heads, \
+                       f, hf, concat, negative_slope, drop, dwh, ld_dwh, partials)
+#define GAT_BS_U(G)                      \
+    case G:                              \
+        if (u == 4) { GAT_BS(G, 4); }    \
+        else { GAT_BS(G, 8); }           \
+        break;
+    switch (g) {
+        GAT_BS_U(1) GAT_BS_U(2) GAT_BS_U(4) GAT_BS_U(8) GAT_BS_U(16) GAT_BS_U(32) GAT_BS_U(64)
+        default: return GAT_EUNSUPPORTED;
+    }
+#undef GAT_BS_U
+#undef GAT_BS
     return status_of(hipGetLastError());
 }
 
 int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_order,
                            int row_begin, int row_end, const int* csr_to_csc, const float* wh,
-                           int ld_wh, const float* s_src, int ld_s, const float* s_dst,
-                           const float* lse, const float* y_heads, const float* grad_out,
-                           int heads, int f, int concat, int score_act, float act_param,
-                           float dropout_p, unsigned long long seed, float* ds_dst,
-                           float* alpha_csc, float* dz_csc, void* stream) {
+                           int ld_wh, const float* s_src, int ld_s, const float* a_src,
+                           const float* c_src, const float* s_dst, const float* lse,
+                           const float* y_heads, const float* grad_out, int heads, int f,
+                           int concat, int score_act, float act_param, float dropout_p,
+                           unsigned long long seed, float* ds_dst, float* az_csc,
+                           int edges_per_row_hint, void* stream) {
     if (score_act < GAT_ACT_LEAKY_RELU || score_act > GAT_ACT_HEAD_SOFTMAX) return GAT_EINVAL;
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     const int hf = heads * f;
@@ -1660,14 +2233,43 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
     if (rows == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
     const DropArgs drop = make_drop(dropout_p, seed);
+    float2* az = reinterpret_cast<float2*>(az_csc);
+    const int hl = f / 4;
+    const bool grp_ok = score_act == GAT_ACT_LEAKY_RELU && act_param >= 0.f && act_param <= 1.f &&
+                        f % 4 == 0 && next_pow2(hl) == hl && a_src != nullptr &&
+                        c_src != nullptr && (ld_wh & 3) == 0 &&
+                        kernel_choice("GAT_BWD_KERNEL", "group", "generic");
+    if (grp_ok) {
+        const int g = next_pow2(hf / 4);
+        const int u = edges_per_row_hint > 0 && edges_per_row_hint <= 12 ? 4 : 8;
+        const long long threads = (long long)rows * g;
+        const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+#define GAT_BWD_GRP(G, UU)                                                                    \
+    hipLaunchKernelGGL((k_edge_bwd_grp<G, UU>), grid, block, 0, st, rowptr, col, row_order,   \
+                       row_begin, row_end, csr_to_csc, wh, ld_wh, a_src, c_src, s_dst, lse,   \
+                       y_heads, grad_out, heads, f, hf, concat, act_param, drop, ds_dst, az)
+#define GAT_BWD_GRP_U(G)                       \
+    case G:                                    \
+        if (u == 4) { GAT_BWD_GRP(G, 4); }     \
+        else { GAT_BWD_GRP(G, 8); }            \
+        break;
+        switch (g) {
+            GAT_BWD_GRP_U(1) GAT_BWD_GRP_U(2) GAT_BWD_GRP_U(4) GAT_BWD_GRP_U(8)
+            GAT_BWD_GRP_U(16) GAT_BWD_GRP_U(32) GAT_BWD_GRP_U(64)
+            default: return GAT_EUNSUPPORTED;
+        }
+#undef GAT_BWD_GRP_U
+#undef GAT_BWD_GRP
+        return status_of(hipGetLastError());
+    }
+    if (s_src == nullptr) return GAT_EINVAL;
     const dim3 grid(rows), block(kWave);
 #define GAT_BWD_ROWS(P)                                                                       \
     case P:                                                                                   \
         hipLaunchKernelGGL((k_edge_bwd_rows<P>), grid, block, 0, st, rowptr, col, row_order,  \
                            row_begin, row_end, csr_to_csc, wh, ld_wh, s_src, ld_s, s_dst, lse, \
                            y_heads, grad_out, heads, f, hf, concat, score_act, act_param,     \
-                           drop,                                                              \
-                           ds_dst, alpha_csc, dz_csc);                                        \
+                           drop, ds_dst, az);                                                 \
         break;
     switch (next_pow2(heads)) {
         GAT_BWD_ROWS(1) GAT_BWD_ROWS(2) GAT_BWD_ROWS(4) GAT_BWD_ROWS(8)
@@ -1679,8 +2281,8 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
 }
 
 int gat_src_backward(const int* csc_ptr, const int* csc_dst, int num_nodes, const float* wh,
-                     int ld_wh, const float* grad_out, const float* alpha_csc,
-                     const float* dz_csc, const float* ds_dst, const float* a_src,
+                     int ld_wh, const float* grad_out, const float* az_csc,
+                     const float* ds_dst, const float* a_src,
                      const float* a_dst, int heads, int f, int concat, float* dwh, int ld_dwh,
                      float* ds_src, float* partials, int num_parts, void* stream) {
     if (heads <= 0 || f <= 0 || num_nodes < 0 || num_parts <= 0) return GAT_EINVAL;
@@ -1692,7 +2294,8 @@ int gat_src_backward(const int* csc_ptr, const int* csc_dst, int num_nodes, cons
     const int cq = (hf + kWave - 1) / kWave;
 #define GAT_SRC_LAUNCH(CQ, P)                                                                 \
     hipLaunchKernelGGL((k_src_bwd<CQ, P>), grid, block, 0, st, csc_ptr, csc_dst, num_nodes,   \
-                       wh, ld_wh, grad_out, alpha_csc, dz_csc, ds_dst, a_src, a_dst, heads, f, \
+                       wh, ld_wh, grad_out, reinterpret_cast<const float2*>(az_csc), ds_dst,   \
+                       a_src, a_dst, heads, f,                                                 \
                        hf, concat, dwh, ld_dwh, ds_src, partials)
 #define GAT_SRC_HP(CQ)                                               \
     switch (next_pow2(heads)) {                                      \
@@ -1714,6 +2317,61 @@ int gat_src_backward(const int* csc_ptr, const int* csc_dst, int num_nodes, cons
     }
 #undef GAT_SRC_HP
 #undef GAT_SRC_LAUNCH
+    return status_of(hipGetLastError());
+}
+
+int gat_weight_grad_workspace_size(int num_nodes, int fin, int hf, size_t* bytes) {
+    if (num_nodes < 0 || fin <= 0 || hf <= 0 || bytes == nullptr) return GAT_EINVAL;
+    *bytes = (size_t)wgrad_chunks(num_nodes, fin, hf) * hf * fin * sizeof(float);
+    return GAT_OK;
+}
+
+int gat_weight_grad(const float* x, int num_nodes, int fin, const float* dwh, int ld_dwh, int hf,
+                    float* dw, void* workspace, size_t workspace_bytes, void* stream) {
+    if (num_nodes < 0 || fin <= 0 || hf <= 0 || ld_dwh < hf) return GAT_EINVAL;
+    size_t need = 0;
+    int rc = gat_weight_grad_workspace_size(num_nodes, fin, hf, &need);
+    if (rc != GAT_OK) return rc;
+    if (workspace_bytes < need) return GAT_EWORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    if (num_nodes == 0) return status_of(hipMemsetAsync(dw, 0, sizeof(float) * hf * fin, st));
+    const int chunks = wgrad_chunks(num_nodes, fin, hf);
+    const int rows = (num_nodes + chunks - 1) / chunks;
+    float* part = (float*)workspace;
+    const dim3 grid((fin + 63) / 64, chunks, (hf + 63) / 64), block(256);
+    hipLaunchKernelGGL(k_wgrad, grid, block, 0, st, dwh, ld_dwh, x, num_nodes, fin, hf, rows,
+                       part);
+    const long long count = (long long)hf * fin;
+    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((count + 15) / 16)), dim3(256), 0, st, part,
+                       chunks, count, dw, chunks);
+    return status_of(hipGetLastError());
+}
+
+int gat_sum_partials_workspace_size(int num_parts, long long width, size_t* bytes) {
+    if (num_parts <= 0 || width <= 0 || bytes == nullptr) return GAT_EINVAL;
+    *bytes = num_parts > 256 ? (size_t)((num_parts + 255) / 256) * width * sizeof(float) : 0;
+    return GAT_OK;
+}
+
+int gat_sum_partials(const float* partials, int num_parts, long long width, float* out,
+                     void* workspace, size_t workspace_bytes, void* stream) {
+    size_t need = 0;
+    const int rc = gat_sum_partials_workspace_size(num_parts, width, &need);
+    if (rc != GAT_OK) return rc;
+    if (workspace_bytes < need) return GAT_EWORKSPACE;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 gx((unsigned)((width + 15) / 16));
+    if (num_parts <= 256) {
+        hipLaunchKernelGGL(k_colsum, gx, dim3(256), 0, st, partials, num_parts, width, out,
+                           num_parts);
+        return status_of(hipGetLastError());
+    }
+    // two stages: sums of 256-row blocks, then of the block sums (fixed order)
+    const int blocks = (num_parts + 255) / 256;
+    float* tmp = (float*)workspace;
+    hipLaunchKernelGGL(k_colsum, dim3(gx.x, blocks), dim3(256), 0, st, partials, num_parts,
+                       width, tmp, 256);
+    hipLaunchKernelGGL(k_colsum, gx, dim3(256), 0, st, tmp, blocks, width, out, blocks);
     return status_of(hipGetLastError());
 }
 

@@ -100,6 +100,7 @@ class CSCGraph(NamedTuple):
     the backward pass reduces each source row's gradient over its out-edges."""
     ptr: torch.Tensor  # int32 [N+1], first CSC slot per source node
     dst: torch.Tensor  # int32 [E'], target row per CSC slot
+    eid: torch.Tensor  # int32 [E'], CSR position per CSC slot
     csr_to_csc: torch.Tensor  # int32 [E'], CSC slot of each CSR position
 
 
@@ -108,14 +109,14 @@ def build_csc(csr: CSRGraph) -> CSCGraph:
     dev = csr.rowptr.device
     n, nnz = csr.num_nodes, csr.num_edges
     ptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
-    dst = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
-    c2c = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    idx = torch.empty(3, max(nnz, 1), dtype=torch.int32, device=dev)
     ws = torch.empty(_lib.csc_workspace_size(nnz, n), dtype=torch.uint8, device=dev)
     _lib.check(lib.gat_csc_build(csr.rowptr.data_ptr(), csr.col.data_ptr(), n, nnz,
-                                 ptr.data_ptr(), dst.data_ptr(), c2c.data_ptr(), ws.data_ptr(),
-                                 ws.numel(), torch.cuda.current_stream(dev).cuda_stream),
+                                 ptr.data_ptr(), idx[0].data_ptr(), idx[1].data_ptr(),
+                                 idx[2].data_ptr(), ws.data_ptr(), ws.numel(),
+                                 torch.cuda.current_stream(dev).cuda_stream),
                "gat_csc_build")
-    return CSCGraph(ptr, dst, c2c)
+    return CSCGraph(ptr, idx[0], idx[1], idx[2])
 
 
 _csc_cache = {}

@@ -261,6 +261,7 @@ class GraphAttentionLayer(torch.nn.Module):
         width = output_channels * num_heads if concat else output_channels
         self.bias = torch.nn.Parameter(torch.zeros(width))
         self._packed: Optional[PackedParams] = None
+        self._bind_packed()
 
     @property
     def negative_slope(self) -> float:
@@ -271,9 +272,44 @@ class GraphAttentionLayer(torch.nn.Module):
         replacing the module after construction takes effect as in the reference)."""
         return score_activation_code(self.attention_relu)
 
-    def packed(self) -> PackedParams:
-        self._packed = pack_params(self, self._packed)
+    def _bind_packed(self) -> PackedParams:
+        """Make the 6H per-head parameters views into six packed buffers — W
+        [H*F, Fin], b, a_src, a_dst [H*F], c_src, c_dst [H] — the layout the
+        kernels read, so no forward concatenates parameters and the backward
+        returns views of packed gradients.  Values, shapes, dtypes and the
+        state_dict are unchanged; optimizers update the views in place."""
+        params = _param_list(self)
+        H, F = self.num_heads, self.output_channels
+        with torch.no_grad():
+            w = torch.cat([p.detach().reshape(F, -1) for p in params[0:H]], 0).contiguous()
+            flat = [torch.cat([p.detach().reshape(-1) for p in params[k * H:(k + 1) * H]])
+                    .contiguous() for k in range(1, 6)]
+        b, a_src, c_src, a_dst, c_dst = flat
+        for h in range(H):
+            params[h].data = w[h * F:(h + 1) * F]
+            params[H + h].data = b[h * F:(h + 1) * F]
+            params[2 * H + h].data = a_src[h * F:(h + 1) * F].view(1, F)
+            params[3 * H + h].data = c_src[h:h + 1]
+            params[4 * H + h].data = a_dst[h * F:(h + 1) * F].view(1, F)
+            params[5 * H + h].data = c_dst[h:h + 1]
+        self._packed = PackedParams(w, b, a_src, c_src, a_dst, c_dst,
+                                    tuple(p.data_ptr() for p in params))
         return self._packed
+
+    def _apply(self, fn, recurse=True):
+        # .to() / .cuda() / .float() replace each parameter's storage: re-pack
+        out = super()._apply(fn, recurse)
+        self._bind_packed()
+        return out
+
+    def packed(self) -> PackedParams:
+        """The packed parameter buffers (re-bound if a parameter was replaced)."""
+        pp = self._packed
+        if pp is None or pp.key != tuple(p.data_ptr() for p in _param_list(self)):
+            pp = self._bind_packed()
+        if pp.w.dtype != torch.float32:
+            raise ValueError(f"parameters must be float32 (the reference's dtype), got {pp.w.dtype}")
+        return pp
 
     def forward(self, x, edge_index):
         x = _check_x(x, self.input_channels)
@@ -287,7 +323,7 @@ class GraphAttentionLayer(torch.nn.Module):
             # training path (training.py): dropout of GAT.py:61 and the HIP backward
             from .training import gat_train_forward, new_dropout_seed
             seed = new_dropout_seed() if p > 0.0 else 0
-            return gat_train_forward(self, x, csr, p, seed)
+            return gat_train_forward(self, x, csr, p, seed, act, act_param)
         return gat_forward(x, csr, self.packed(), self.bias.detach(), self.num_heads,
                            self.output_channels, self.concat, act_param)
 

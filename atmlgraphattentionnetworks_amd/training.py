@@ -9,16 +9,22 @@ PyG's gather/scatter ops (``run_inductive.py:83-90``, ``run_*_experiment.py``:
   forward   gat_project, then gat_edge_aggregate_ex (dropout GAT.py:61 from a
             counter-based hash; any score activation; also stores lse and the
             per-head aggregation y)
-  backward  1. gat_edge_backward_rows (per target row: dropout, softmax and
-               LeakyReLU backward -> ds_dst, and per-edge A / dz in CSC order)
-            2. gat_src_backward (per source row: dWh = sum A * dy + the score
-               terms; per-wave partials of da/dc -- deterministic, no atomics)
-            3. dW = dWh^T x, db = sum dWh, dx = dWh W (hipBLASLt via torch.mm:
-               plain library GEMMs), dbias = sum of the incoming gradient.
+  backward  1. gat_bwd_targets (per target row: dropout, softmax and LeakyReLU
+               backward -> ds_dst, and a per-target table [g | s_dst, lse, delta])
+            2. gat_bwd_sources (per source row over the CSC: recomputes each
+               edge's coefficient from the table, dWh = sum A * dy + the score
+               terms; per-wave partials of da/dc/db/dbias -- deterministic, no
+               atomics), gat_sum_partials
+            (other score activations or head widths: gat_edge_backward_rows,
+            which stores (A, dz) per edge in CSC order, + gat_src_backward)
+            3. gat_weight_grad: dW = dWh^T x (split-K fp32 MFMA)
+            4. dx = dWh W (hipBLASLt via torch.mm, a plain library GEMM), only
+               when x needs a gradient.
 
-The packed parameters (W = cat of ws[h].weight, ...) are built with
-differentiable ``torch.cat`` by the caller, so the gradients land on each
-head's ``Linear`` exactly where the reference's would.
+The per-head parameters are views into the packed buffers the kernels read
+(``GraphAttentionLayer._bind_packed``), so the gradients come back as views of
+the packed gradients and land on each head's ``Linear`` exactly where the
+reference's autograd would put them.
 """
 from __future__ import annotations
 
@@ -40,109 +46,196 @@ def new_dropout_seed() -> int:
 
 
 class GATFunction(torch.autograd.Function):
-    """Layer forward (training) and backward on prepared inputs."""
+    """Layer forward (training) and backward on prepared inputs.
+
+    ``params`` are the layer's 6H per-head leaves, in ``_param_list`` order;
+    they only route gradients — the kernels read the packed buffers ``pp``
+    they are views of (``GraphAttentionLayer._bind_packed``)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, a_src, c_src, a_dst, c_dst, bias, csr: CSRGraph, heads: int,
-                f: int, concat: bool, act: int, act_param: float, p: float, seed: int):
+    def forward(ctx, x, bias, cfg, csr: CSRGraph, pp, *params):
+        heads, f, concat, act, act_param, p, seed = cfg
         lib = _lib.load()
         n, fin = x.shape
         hf = heads * f
         hfp = (hf + 3) // 4 * 4
         dev = x.device
         stream = torch._C._cuda_getCurrentRawStream(dev.index)
-        wh = torch.empty(n, hfp, dtype=torch.float32, device=dev)
-        s_src = torch.empty(n, heads, dtype=torch.float32, device=dev)
-        s_dst = torch.empty(n, heads, dtype=torch.float32, device=dev)
-        _lib.check(lib.gat_project(x.data_ptr(), n, fin, w.data_ptr(), b.data_ptr(),
-                                   a_src.data_ptr(), c_src.data_ptr(), a_dst.data_ptr(),
-                                   c_dst.data_ptr(), heads, f, wh.data_ptr(), hfp,
-                                   s_src.data_ptr(), heads, s_dst.data_ptr(), stream),
-                   "gat_project")
+        # one workspace: Wh | s_src | s_dst | lse | y
+        ws = torch.empty(n * (hfp + 3 * heads + hf), dtype=torch.float32, device=dev)
+        wh = ws[:n * hfp].view(n, hfp)
+        o = n * hfp
+        s_src = ws[o:o + n * heads].view(n, heads)
+        s_dst = ws[o + n * heads:o + 2 * n * heads].view(n, heads)
+        lse = ws[o + 2 * n * heads:o + 3 * n * heads].view(n, heads)
+        y = ws[o + 3 * n * heads:].view(n, hf)
+        rc = lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                             pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
+                             pp.c_dst.data_ptr(), heads, f, wh.data_ptr(), hfp,
+                             s_src.data_ptr(), heads, s_dst.data_ptr(), stream)
+        if rc:
+            _lib.check(rc, "gat_project")
         out = torch.empty(n, hf if concat else f, dtype=torch.float32, device=dev)
-        lse = torch.empty(n, heads, dtype=torch.float32, device=dev)
-        y = torch.empty(n, hf, dtype=torch.float32, device=dev)
         order = csr.order
-        _lib.check(lib.gat_edge_aggregate_ex(
+        rc = lib.gat_edge_aggregate_ex(
             csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
-            0, n, wh.data_ptr(), hfp, s_src.data_ptr(), heads, a_src.data_ptr(),
-            c_src.data_ptr(), s_dst.data_ptr(), heads, f, int(concat), int(act),
-            float(act_param), float(p), int(seed), bias.data_ptr(), out.data_ptr(),
-            lse.data_ptr(), y.data_ptr(), csr.num_edges // max(n, 1), stream),
-            "gat_edge_aggregate_ex")
-        ctx.save_for_backward(x, w, a_src, a_dst, wh, s_src, s_dst, lse, y)
-        ctx.csr = csr
-        ctx.cfg = (heads, f, bool(concat), int(act), float(act_param), float(p), int(seed))
+            0, n, wh.data_ptr(), hfp, s_src.data_ptr(), heads, pp.a_src.data_ptr(),
+            pp.c_src.data_ptr(), s_dst.data_ptr(), heads, f, int(concat), act, act_param, p,
+            seed, bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(),
+            csr.num_edges // max(n, 1), stream)
+        if rc:
+            _lib.check(rc, "gat_edge_aggregate_ex")
+        ctx.save_for_backward(x, ws)
+        ctx.csr, ctx.pp, ctx.cfg = csr, pp, cfg
         return out
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, g):
-        x, w, a_src, a_dst, wh, s_src, s_dst, lse, y = ctx.saved_tensors
+        x, ws = ctx.saved_tensors
         heads, f, concat, act, act_param, p, seed = ctx.cfg
-        csr = ctx.csr
-        lib = _lib.load()
+        csr, pp = ctx.csr, ctx.pp
         g = g.contiguous()
         if g.dtype != torch.float32:
             g = g.float()
         n, fin = x.shape
         hf = heads * f
-        hfp = wh.size(1)
         dev = x.device
         stream = torch._C._cuda_getCurrentRawStream(dev.index)
         csc = get_csc(csr)
-        nnz = csr.num_edges
-        ds_dst = torch.empty(n, heads, dtype=torch.float32, device=dev)
-        alpha = torch.empty(max(nnz, 1), heads, dtype=torch.float32, device=dev)
-        dz = torch.empty(max(nnz, 1), heads, dtype=torch.float32, device=dev)
-        order = csr.order
-        _lib.check(lib.gat_edge_backward_rows(
-            csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
-            0, n, csc.csr_to_csc.data_ptr(), wh.data_ptr(), hfp, s_src.data_ptr(), heads,
-            s_dst.data_ptr(), lse.data_ptr(), y.data_ptr(), g.data_ptr(), heads, f, int(concat),
-            act, act_param, p, seed, ds_dst.data_ptr(), alpha.data_ptr(), dz.data_ptr(), stream),
-            "gat_edge_backward_rows")
-        parts = max(1, min(n, _MAX_PARTS))
-        dwh = torch.empty(n, hf, dtype=torch.float32, device=dev)
-        part = torch.empty(parts, 2 * hf + 2 * heads, dtype=torch.float32, device=dev)
-        _lib.check(lib.gat_src_backward(
-            csc.ptr.data_ptr(), csc.dst.data_ptr(), n, wh.data_ptr(), hfp, g.data_ptr(),
-            alpha.data_ptr(), dz.data_ptr(), ds_dst.data_ptr(), a_src.data_ptr(),
-            a_dst.data_ptr(), heads, f, int(concat), dwh.data_ptr(), hf, 0, part.data_ptr(),
-            parts, stream), "gat_src_backward")
-        ps = part.sum(0)
+        dwh, ps = _backward_recompute(ctx, g, ws, csc, stream)
+        if dwh is None:
+            dwh, ps = _backward_stored(ctx, g, ws, csc, stream)
         need = ctx.needs_input_grad
-        dx = torch.mm(dwh, w) if need[0] else None
-        dw = torch.mm(dwh.t(), x) if need[1] else None
-        db = dwh.sum(0) if need[2] else None
-        da_src = ps[:hf] if need[3] else None
-        dc_src = ps[2 * hf:2 * hf + heads] if need[4] else None
-        da_dst = ps[hf:2 * hf] if need[5] else None
-        dc_dst = ps[2 * hf + heads:] if need[6] else None
-        dbias = g.sum(0) if need[7] else None
-        return (dx, dw, db, da_src, dc_src, da_dst, dc_dst, dbias,
-                None, None, None, None, None, None, None, None)
+        dx = torch.mm(dwh, pp.w) if need[0] else None
+        dbias = ps[3 * hf + 2 * heads:] if need[1] else None
+        grads = [None] * (6 * heads)
+        if any(need[5:]):
+            lib = _lib.load()
+            dw = torch.empty(hf, fin, dtype=torch.float32, device=dev)
+            wsz = _lib.weight_grad_workspace_size(n, fin, hf)
+            wws = torch.empty(max(wsz // 4, 1), dtype=torch.float32, device=dev)
+            rc = lib.gat_weight_grad(x.data_ptr(), n, fin, dwh.data_ptr(), hf, hf, dw.data_ptr(),
+                                     wws.data_ptr(), wsz, stream)
+            if rc:
+                _lib.check(rc, "gat_weight_grad")
+            H = heads
+            grads[0:H] = dw.view(H, f, fin).unbind(0)
+            grads[H:2 * H] = ps[2 * hf + 2 * H:3 * hf + 2 * H].view(H, f).unbind(0)
+            grads[2 * H:3 * H] = ps[:hf].view(H, 1, f).unbind(0)
+            grads[3 * H:4 * H] = ps[2 * hf:2 * hf + H].view(H, 1).unbind(0)
+            grads[4 * H:5 * H] = ps[hf:2 * hf].view(H, 1, f).unbind(0)
+            grads[5 * H:6 * H] = ps[2 * hf + H:2 * hf + 2 * H].view(H, 1).unbind(0)
+        return (dx, dbias, None, None, None, *grads)
 
 
-def packed_params_differentiable(layer):
-    """cat of the per-head parameters, recorded by autograd (GAT.py:19-22)."""
-    H = layer.num_heads
-    ws = list(layer.ws._modules.values())
-    a1 = list(layer.attentions1._modules.values())
-    a2 = list(layer.attentions2._modules.values())
-    w = torch.cat([m.weight for m in ws], 0)
-    b = torch.cat([m.bias for m in ws], 0)
-    a_src = torch.cat([m.weight.reshape(-1) for m in a1])
-    c_src = torch.cat([m.bias.reshape(-1) for m in a1])
-    a_dst = torch.cat([m.weight.reshape(-1) for m in a2])
-    c_dst = torch.cat([m.bias.reshape(-1) for m in a2])
-    assert w.size(0) == H * layer.output_channels
-    return w, b, a_src, c_src, a_dst, c_dst
+def _saved_layout(ctx, ws):
+    """Pointers into the forward workspace: Wh | s_src | s_dst | lse | y."""
+    heads, f = ctx.cfg[0], ctx.cfg[1]
+    n = ctx.csr.num_nodes
+    hfp = (heads * f + 3) // 4 * 4
+    p_wh = ws.data_ptr()
+    p_ss = p_wh + 4 * n * hfp
+    return hfp, p_wh, p_ss, p_ss + 4 * n * heads, p_ss + 8 * n * heads, p_ss + 12 * n * heads
 
 
-def gat_train_forward(layer, x: torch.Tensor, csr: CSRGraph, p: float, seed: int):
-    w, b, a_src, c_src, a_dst, c_dst = packed_params_differentiable(layer)
-    act, act_param = layer.score_activation()
-    return GATFunction.apply(x, w, b, a_src, c_src, a_dst, c_dst, layer.bias, csr,
-                             layer.num_heads, layer.output_channels, layer.concat,
-                             act, act_param, p, seed)
+def _backward_recompute(ctx, g, ws, csc, stream):
+    """gat_bwd_targets + gat_bwd_sources (no per-edge intermediates); returns
+    (None, None) when the shape or activation needs the stored-coefficient path."""
+    heads, f, concat, act, act_param, p, seed = ctx.cfg
+    if act != _lib.GAT_ACT_LEAKY_RELU:
+        return None, None
+    csr, pp = ctx.csr, ctx.pp
+    lib = _lib.load()
+    n = csr.num_nodes
+    hf = heads * f
+    ldg = hf if concat else f
+    pw = 3 * hf + 2 * heads + ldg
+    ld_t = _lib.bwd_table_layout(heads, f, concat)
+    parts = _lib.bwd_sources_parts(n, heads, f)
+    sws = (parts + 255) // 256 * pw if parts > 256 else 0
+    hfp, p_wh, p_ss, p_sd, p_lse, p_y = _saved_layout(ctx, ws)
+    # one workspace: ds_dst | target table | dwh | partials | sums | scratch
+    o_t = (n * heads + 3) // 4 * 4
+    o_dwh = o_t + n * ld_t
+    o_part = o_dwh + n * hf
+    o_ps = o_part + parts * pw
+    bw = torch.empty(o_ps + pw + sws, dtype=torch.float32, device=g.device)
+    base = bw.data_ptr()
+    order = csr.order
+    hint = csr.num_edges // max(n, 1)
+    rc = lib.gat_bwd_targets(
+        csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(), 0,
+        n, p_wh, hfp, pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, p_lse, p_y, g.data_ptr(),
+        heads, f, int(concat), act_param, p, seed, base, base + 4 * o_t, ld_t, hint, stream)
+    if rc == _lib.GAT_EUNSUPPORTED:
+        return None, None
+    if rc:
+        _lib.check(rc, "gat_bwd_targets")
+    rc = lib.gat_bwd_sources(
+        csc.ptr.data_ptr(), csc.dst.data_ptr(), csc.eid.data_ptr(), n, p_wh, hfp,
+        base + 4 * o_t, ld_t, base, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+        pp.a_dst.data_ptr(), heads, f, int(concat), act_param, p, seed, base + 4 * o_dwh, hf,
+        base + 4 * o_part, parts, hint, stream)
+    if rc:
+        _lib.check(rc, "gat_bwd_sources")
+    rc = lib.gat_sum_partials(base + 4 * o_part, parts, pw, base + 4 * o_ps,
+                              base + 4 * (o_ps + pw), 4 * sws, stream)
+    if rc:
+        _lib.check(rc, "gat_sum_partials")
+    return bw[o_dwh:o_part].view(n, hf), bw[o_ps:o_ps + pw]
+
+
+def _backward_stored(ctx, g, ws, csc, stream):
+    """gat_edge_backward_rows (per-edge (A, dz) stored in CSC order) +
+    gat_src_backward: any score activation, any head width."""
+    heads, f, concat, act, act_param, p, seed = ctx.cfg
+    csr, pp = ctx.csr, ctx.pp
+    lib = _lib.load()
+    n = csr.num_nodes
+    hf = heads * f
+    nnz = csr.num_edges
+    ldg = hf if concat else f
+    parts = max(1, min(n, _MAX_PARTS))
+    pw = 3 * hf + 2 * heads + ldg
+    sws = (parts + 255) // 256 * pw if parts > 256 else 0
+    hfp, p_wh, p_ss, p_sd, p_lse, p_y = _saved_layout(ctx, ws)
+    # one workspace: ds_dst | (A, dz) per edge and head | dwh | partials | sums | scratch
+    m = 2 * max(nnz, 1) * heads
+    o_dwh = n * heads + m
+    o_part = o_dwh + n * hf
+    o_ps = o_part + parts * pw
+    bw = torch.empty(o_ps + pw + sws, dtype=torch.float32, device=g.device)
+    p_dsd = bw.data_ptr()
+    p_az = p_dsd + 4 * n * heads
+    p_part = bw.data_ptr() + 4 * o_part
+    order = csr.order
+    rc = lib.gat_edge_backward_rows(
+        csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
+        0, n, csc.csr_to_csc.data_ptr(), p_wh, hfp, p_ss, heads, pp.a_src.data_ptr(),
+        pp.c_src.data_ptr(), p_sd, p_lse, p_y, g.data_ptr(), heads, f, int(concat), act,
+        act_param, p, seed, p_dsd, p_az, nnz // max(n, 1), stream)
+    if rc:
+        _lib.check(rc, "gat_edge_backward_rows")
+    rc = lib.gat_src_backward(
+        csc.ptr.data_ptr(), csc.dst.data_ptr(), n, p_wh, hfp, g.data_ptr(), p_az, p_dsd,
+        pp.a_src.data_ptr(), pp.a_dst.data_ptr(), heads, f, int(concat),
+        bw.data_ptr() + 4 * o_dwh, hf, 0, p_part, parts, stream)
+    if rc:
+        _lib.check(rc, "gat_src_backward")
+    rc = lib.gat_sum_partials(p_part, parts, pw, bw.data_ptr() + 4 * o_ps,
+                              bw.data_ptr() + 4 * (o_ps + pw), 4 * sws, stream)
+    if rc:
+        _lib.check(rc, "gat_sum_partials")
+    return bw[o_dwh:o_part].view(n, hf), bw[o_ps:o_ps + pw]
+
+
+def gat_train_forward(layer, x: torch.Tensor, csr: CSRGraph, p: float, seed: int,
+                      act: int = None, act_param: float = None):
+    from .layer import _param_list
+    if act is None:
+        act, act_param = layer.score_activation()
+    pp = layer.packed()
+    cfg = (layer.num_heads, layer.output_channels, bool(layer.concat), int(act),
+           float(act_param), float(p), int(seed))
+    return GATFunction.apply(x, layer.bias, cfg, csr, pp, *_param_list(layer))

@@ -172,48 +172,119 @@ int gat_csc_workspace_size(long long nnz, int num_nodes, size_t* bytes);
  *   rowptr/col  from gat_csr_build; nnz = rowptr[num_nodes]
  *   csc_ptr     [num_nodes + 1] int32: first CSC slot of each source node
  *   csc_dst     [nnz] int32: target row of the edge in each CSC slot
- *   csr_to_csc  [nnz] int32: CSC slot of each CSR position
+ *   csc_eid     optional [nnz] int32: CSR position of the edge in each CSC slot
+ *               (gat_bwd_sources needs it when dropout is on)
+ *   csr_to_csc  optional [nnz] int32: CSC slot of each CSR position
+ *               (gat_edge_backward_rows needs it)
  * Within a source, slots follow CSR order (stable), so reductions over them are
  * deterministic.
  */
 int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nnz, int* csc_ptr,
-                  int* csc_dst, int* csr_to_csc, void* workspace, size_t workspace_bytes,
-                  void* stream);
+                  int* csc_dst, int* csc_eid, int* csr_to_csc, void* workspace,
+                  size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward, recompute form (LeakyReLU with slope in [0, 1], f % 4 == 0 and f/4 a
+ * power of two; GAT_EUNSUPPORTED otherwise — then use gat_edge_backward_rows +
+ * gat_src_backward).  No per-edge intermediate is stored: pass 2 recomputes each
+ * edge's coefficient from a per-target table written by pass 1.
+ * ------------------------------------------------------------------------- */
+
+/* Row stride (floats) of the target table: round_up(ldg, 4) + 4*heads,
+ * ldg = heads*f if concat else f. */
+int gat_bwd_table_layout(int heads, int f, int concat, int* ld_t);
+
+/*
+ * Pass 1, per TARGET row: dL/ds_dst and the target table
+ *   table[i] = [grad_out[i] (ldg) | pad | per head (s_dst, lse, delta, 0)],
+ * delta = dy_h . y_h.  Inputs as gat_edge_backward_rows (a_src/c_src required).
+ */
+int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int row_begin,
+                    int row_end, const float* wh, int ld_wh, const float* a_src,
+                    const float* c_src, const float* s_dst, const float* lse,
+                    const float* y_heads, const float* grad_out, int heads, int f, int concat,
+                    float negative_slope, float dropout_p, unsigned long long seed,
+                    float* ds_dst, float* table, int ld_t, int edges_per_row_hint,
+                    void* stream);
+
+/* Number of partial rows gat_bwd_sources writes for this shape (a multiple of 4). */
+int gat_bwd_sources_parts(int num_nodes, int heads, int f, int* num_parts);
+
+/*
+ * Pass 2, per SOURCE row (over the CSC): dwh (as gat_src_backward) and the
+ * partials [num_parts, 3*heads*f + 2*heads + ldg] in gat_src_backward's layout.
+ *   table, ld_t   from gat_bwd_targets; ds_dst from gat_bwd_targets
+ *   csc_eid       required when dropout_p > 0 (the mask is keyed on CSR positions)
+ *   num_parts     from gat_bwd_sources_parts
+ */
+int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, int num_nodes,
+                    const float* wh, int ld_wh, const float* table, int ld_t,
+                    const float* ds_dst, const float* a_src, const float* c_src,
+                    const float* a_dst, int heads, int f, int concat, float negative_slope,
+                    float dropout_p, unsigned long long seed, float* dwh, int ld_dwh,
+                    float* partials, int num_parts, int edges_per_row_hint, void* stream);
 
 /*
  * Backward pass 1, per TARGET row (softmax + LeakyReLU + dropout backward).
  *   grad_out   dL/d(layer output) [rows, heads*f] (concat) or [rows, f] (mean)
  *   lse, y_heads  as written by gat_edge_aggregate_ex (same activation, seed, dropout_p)
  *   s_src      as written by gat_project
+ *   a_src, c_src  optional (the attentions1 parameters): with LeakyReLU and f/4 a
+ *              power of two the library recomputes s_src from the gathered Wh row
+ *   edges_per_row_hint  as for gat_edge_aggregate
  * Writes:
- *   ds_dst     [rows, heads]  dL/ds_dst
- *   alpha_csc  [nnz, heads]   coefficient used in the forward (after dropout), at
- *                             each edge's CSC slot
- *   dz_csc     [nnz, heads]   dL/d(s_dst[i] + s_src[j]) per edge, at its CSC slot
+ *   ds_dst     [rows, heads]     dL/ds_dst
+ *   az_csc     [nnz, heads, 2]   per edge and head, at the edge's CSC slot:
+ *                                (A, dz) = (coefficient used in the forward, after
+ *                                dropout; dL/d(s_dst[i] + s_src[j]))
  */
 int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_order,
                            int row_begin, int row_end, const int* csr_to_csc, const float* wh,
-                           int ld_wh, const float* s_src, int ld_s, const float* s_dst,
-                           const float* lse, const float* y_heads, const float* grad_out,
-                           int heads, int f, int concat, int score_act, float act_param,
-                           float dropout_p, unsigned long long seed, float* ds_dst,
-                           float* alpha_csc, float* dz_csc, void* stream);
+                           int ld_wh, const float* s_src, int ld_s, const float* a_src,
+                           const float* c_src, const float* s_dst, const float* lse,
+                           const float* y_heads, const float* grad_out, int heads, int f,
+                           int concat, int score_act, float act_param, float dropout_p,
+                           unsigned long long seed, float* ds_dst, float* az_csc,
+                           int edges_per_row_hint, void* stream);
 
 /*
  * Backward pass 2, per SOURCE row: message backward plus the score terms.
  *   dwh[j]     = sum_{edges j->i} alpha * dy[i]  +  ds_src[j,h] a_src_h + ds_dst[j,h] a_dst_h
  *                ([num_nodes, ld_dwh], columns [0, heads*f)) = dL/dWh
  *   ds_src     optional [num_nodes, heads] = dL/ds_src
- *   partials   [num_parts, 2*heads*f + 2*heads]: per-part sums of
- *              [ds_src*Wh (da_src) | ds_dst*Wh (da_dst) | ds_src (dc_src) | ds_dst (dc_dst)];
+ *   partials   [num_parts, 3*heads*f + 2*heads + ldg] (ldg = heads*f if concat else f):
+ *              per-part sums of [ds_src*Wh (da_src) | ds_dst*Wh (da_dst) | ds_src (dc_src) |
+ *              ds_dst (dc_dst) | dwh rows (d of gat_project's b) | grad_out rows (dbias)];
  *              the caller sums them over parts (deterministic, no atomics).
  *   num_parts  >= 1; rows are strided over parts (a good value: min(num_nodes, 8192))
  */
 int gat_src_backward(const int* csc_ptr, const int* csc_dst, int num_nodes, const float* wh,
-                     int ld_wh, const float* grad_out, const float* alpha_csc,
-                     const float* dz_csc, const float* ds_dst, const float* a_src,
+                     int ld_wh, const float* grad_out, const float* az_csc,
+                     const float* ds_dst, const float* a_src,
                      const float* a_dst, int heads, int f, int concat, float* dwh, int ld_dwh,
                      float* ds_src, float* partials, int num_parts, void* stream);
+
+/* Workspace bytes gat_weight_grad needs. */
+int gat_weight_grad_workspace_size(int num_nodes, int fin, int hf, size_t* bytes);
+
+/*
+ * Weight gradient of gat_project: dw[hf, fin] = dwh^T x (hf = heads*f), the
+ * gradient of cat_h ws[h].weight (GAT.py:20).  Split-K fp32 MFMA over the node
+ * rows with a fixed-order reduction (deterministic).
+ *   x    [num_nodes, fin], dwh [num_nodes, ld_dwh] (gat_src_backward's dwh)
+ */
+int gat_weight_grad(const float* x, int num_nodes, int fin, const float* dwh, int ld_dwh, int hf,
+                    float* dw, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Workspace bytes gat_sum_partials needs (0 for num_parts <= 256). */
+int gat_sum_partials_workspace_size(int num_parts, long long width, size_t* bytes);
+
+/*
+ * out[e] = sum over p of partials[p * width + e] (fixed summation order, so
+ * deterministic): reduces gat_src_backward's per-part partials.
+ */
+int gat_sum_partials(const float* partials, int num_parts, long long width, float* out,
+                     void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -31,6 +31,7 @@ CASES = [
     (150, 900, 12, 3, 5, True),      # generic, odd sizes
     (128, 1000, 32, 6, 32, True),    # HF = 192: three columns per lane
     (64, 400, 16, 2, 128, False),    # HF = 256
+    (700, 5000, 150, 8, 8, True),    # Fin = 150: three fin tiles in the weight gradient
 ]
 
 
@@ -105,9 +106,16 @@ def _check_grads(layer, state, xd, out, ei, x, H, concat, gout, drop=None):
         _close(k, got[k].grad, g, ref32=r32_dp[k])
 
 
+@pytest.mark.parametrize("kernel", ["default", "stored", "generic"])
 @pytest.mark.parametrize("case", CASES, ids=[f"n{c[0]}_H{c[3]}F{c[4]}_{'cat' if c[5] else 'mean'}"
                                              for c in CASES])
-def test_backward_matches_oracle(case):
+def test_backward_matches_oracle(case, kernel, monkeypatch):
+    """All backward paths: recompute (gat_bwd_targets + gat_bwd_sources, the
+    default where the shape allows it), stored coefficients with the
+    lane-group target kernel (GAT_BWD_KERNEL=stored) and with the generic one
+    (GAT_BWD_KERNEL=generic)."""
+    if kernel != "default":
+        monkeypatch.setenv("GAT_BWD_KERNEL", kernel)
     n, e, fin, H, F, concat = case
     layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat)
     gout = torch.randn(n, H * F if concat else F, generator=torch.Generator().manual_seed(5))
@@ -118,7 +126,10 @@ def test_backward_matches_oracle(case):
 @pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[3], CASES[5]],
                          ids=["H8F8_cat", "H8F8_mean", "H1F7_mean", "H3F5_cat"])
 @pytest.mark.parametrize("p", [0.6, 0.2])
-def test_dropout_forward_and_backward(case, p):
+@pytest.mark.parametrize("kernel", ["default", "stored"])
+def test_dropout_forward_and_backward(case, p, kernel, monkeypatch):
+    if kernel != "default":
+        monkeypatch.setenv("GAT_BWD_KERNEL", kernel)
     n, e, fin, H, F, concat = case
     layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat, seed=3)
     seed = 0x1234_5678_9ABC + int(p * 10)
@@ -198,6 +209,7 @@ def test_csc_build_matches_numpy():
     ptr = np.concatenate([[0], np.cumsum(np.bincount(col, minlength=n))])
     assert np.array_equal(csc.ptr.cpu().numpy(), ptr)
     assert np.array_equal(csc.dst.cpu().numpy()[:nnz], erow[order])
+    assert np.array_equal(csc.eid.cpu().numpy()[:nnz], order)
     c2c = np.empty(nnz, dtype=np.int64)
     c2c[order] = np.arange(nnz)
     assert np.array_equal(csc.csr_to_csc.cpu().numpy()[:nnz], c2c)
@@ -274,3 +286,27 @@ def test_score_activation_forward_and_backward(act, case):
     got = dict(layer.named_parameters())
     for k, g in r_dp.items():
         _close(k, got[k].grad, g, ref32=s_dp[k])
+
+
+def test_params_are_views_of_packed_buffers_after_to_and_step():
+    """_bind_packed: after .to(), optimizer steps and load_state_dict the
+    per-head parameters stay views of the packed buffers the kernels read."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    torch.manual_seed(0)
+    layer = GraphAttentionLayer(12, 4, num_heads=3, concat=True).to(DEV)
+    pp = layer.packed()
+    assert layer.ws[2].weight.data_ptr() == pp.w.data_ptr() + 4 * 8 * 12
+    opt = torch.optim.Adam(layer.parameters(), lr=0.1)
+    x = torch.randn(50, 12, device=DEV)
+    ei = _graph(50, 300, 1).to(DEV)
+    layer(x, ei).sum().backward()
+    opt.step()
+    assert layer.packed() is pp
+    assert torch.equal(pp.w[8:12], layer.ws[2].weight)
+    sd = {k: v.clone() + 1 for k, v in layer.state_dict().items()}
+    layer.load_state_dict(sd)
+    assert layer.packed() is pp and torch.equal(pp.c_dst[1:2], sd["attentions2.1.bias"])
+    # replacing a parameter object re-binds
+    layer.ws[0].weight = torch.nn.Parameter(torch.zeros(4, 12, device=DEV))
+    pp2 = layer.packed()
+    assert pp2 is not pp and torch.equal(pp2.w[:4], torch.zeros(4, 12, device=DEV))
