@@ -84,6 +84,49 @@ def cpu_baseline(layer_state, x, ei, heads, concat, n_edges_total, budget_s: flo
                        f"{threads} threads, {cpu_model()})")}
 
 
+def train_step(layer, x, ei, n_edges: int, steps: int) -> dict:
+    """One training step of the layer: forward in training
+    mode with the layer's attention dropout (0.6, GAT.py:61) and the HIP
+    backward to x and every parameter, with a fixed upstream gradient; timed
+    with events over ``steps`` steps.  Not part of ``value`` (the metric is the
+    eval forward)."""
+    layer.train()
+    xg = x.detach().clone().requires_grad_(True)
+    gout = torch.randn(x.size(0), layer.num_heads * layer.output_channels if layer.concat
+                       else layer.output_channels, device=x.device)
+
+    def one():
+        layer.zero_grad(set_to_none=True)
+        xg.grad = None
+        layer(xg, ei).backward(gout)
+
+    for _ in range(5):
+        one()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    ev0.record(stream)
+    for _ in range(steps):
+        one()
+    ev1.record(stream)
+    ev1.synchronize()
+    step_ms = ev0.elapsed_time(ev1) / steps
+    with torch.no_grad():
+        for _ in range(3):
+            layer(x, ei)
+        ev0.record(stream)
+        for _ in range(steps):
+            layer(x, ei)
+        ev1.record(stream)
+        ev1.synchronize()
+    fwd_ms = ev0.elapsed_time(ev1) / steps
+    layer.eval()
+    return {"what": "layer forward (training mode, attention dropout 0.6) + HIP backward to x "
+                    "and all parameters",
+            "train_step_ms": step_ms, "forward_train_ms": fwd_ms,
+            "backward_ms": step_ms - fwd_ms, "train_edges_per_s": n_edges / (step_ms * 1e-3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,6 +144,8 @@ def main():
                     help="take the torch.distributed path even at WORLD_SIZE=1 (testing)")
     ap.add_argument("--no-strong-probe", action="store_true",
                     help="multi-GPU: skip the strong-scaling all-gather/replicate measurement")
+    ap.add_argument("--no-train", action="store_true",
+                    help="skip the training-step (forward with dropout + backward) measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +234,8 @@ def main():
         ev1.synchronize()
         proj_ms = ev0.elapsed_time(ev1) / args.edge_iters
 
+    training = None if args.no_train else train_step(layer, x, ei, n_edges, args.steps)
+
     alg_bytes = edge_kernel_bytes(n, n_edges, w.heads, w.out_channels, w.concat)
     proj_tflops = 2.0 * n * w.in_channels * w.heads * w.out_channels / (proj_ms * 1e-3) / 1e12
     achieved = alg_bytes / (edge_ms * 1e-3) / 1e9
@@ -219,6 +266,8 @@ def main():
                        "unit": "TFLOP/s", "frac": proj_tflops / MFMA_F32_PEAK_TFLOPS,
                        "kernel": "k_project (fp32 MFMA 16x16x4)"},
     }
+    if training is not None:
+        result["training"] = training
     if not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(layer.state_dict(), x, ei, w.heads, w.concat,
                                               n_edges)
