@@ -21,7 +21,7 @@ from . import _lib
 
 class CSRGraph(NamedTuple):
     rowptr: torch.Tensor  # int32 [N+1]
-    col: torch.Tensor  # int32 [E+N], source node ids, self-loop last per row
+    col: torch.Tensor  # int32 [E+N], source node ids, ascending within each row
     num_nodes: int
     num_edges: int  # E + N (edges after add_self_loops)
     order: Optional[torch.Tensor] = None  # int32 [N], rows by descending in-degree

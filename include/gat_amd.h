@@ -126,8 +126,10 @@ int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);
  *   rowptr     [num_nodes + 1] int32,  col [num_edges + num_nodes] int32
  *   row_order  optional [num_nodes] int32: rows by descending in-degree (stable),
  *              the schedule gat_edge_aggregate takes; may be NULL
- * Within a row the input edge order is kept and the loop comes last, matching
- * cat([edge_index, loops]).  Existing self-loops and multi-edges are kept.
+ * Within a row, sources ascend; equal (target, source) pairs — multi-edges, a
+ * pre-existing self-loop beside the added one — keep cat([edge_index, loops])
+ * order.  Existing self-loops and multi-edges are kept, as add_self_loops keeps
+ * them.  (Only the summation order depends on the order within a row.)
  * *error_flag (device int) is set non-zero if any index is outside [0, num_nodes).
  */
 int gat_csr_build(const long long* edge_index, long long num_edges, int num_nodes, int* rowptr,

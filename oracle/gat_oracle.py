@@ -295,10 +295,11 @@ def dropout_factors(positions, num_heads: int, p: float, seed: int):
 
 def csr_positions(edge_index: torch.Tensor, num_nodes: int):
     """CSR position of each edge of ``add_self_loops(edge_index)`` in the HIP
-    library's CSR (stable sort by target, loops last per row)."""
+    library's CSR (sorted by (target, source); equal pairs in input order)."""
     import numpy as np
     dst = np.concatenate([edge_index[1].cpu().numpy(), np.arange(num_nodes)])
-    order = np.argsort(dst, kind="stable")
+    src = np.concatenate([edge_index[0].cpu().numpy(), np.arange(num_nodes)])
+    order = np.lexsort((src, dst))
     pos = np.empty_like(order)
     pos[order] = np.arange(order.size)
     return pos

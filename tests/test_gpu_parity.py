@@ -134,10 +134,11 @@ def test_csr_bit_exact():
     dst = rng.integers(0, n, size=e)
     ei = torch.from_numpy(np.stack([src, dst]).astype(np.int64))
     csr = build_csr(ei.to(dev()), n)
-    # expected: add_self_loops order (loops last), grouped by target, stable
+    # expected: the edges of add_self_loops (loops appended), sorted by (target,
+    # source), equal pairs in input order (stable)
     s_all = np.concatenate([src, np.arange(n)])
     d_all = np.concatenate([dst, np.arange(n)])
-    order = np.argsort(d_all, kind="stable")
+    order = np.lexsort((s_all, d_all))
     exp_col = s_all[order].astype(np.int32)
     exp_rowptr = np.concatenate([[0], np.cumsum(np.bincount(d_all, minlength=n))]).astype(np.int32)
     assert np.array_equal(csr.rowptr.cpu().numpy(), exp_rowptr)

@@ -78,7 +78,9 @@ def test_dropout_mask_restatement_properties():
     # different seeds and heads decorrelate
     m2 = dropout_factors(np.arange(200000), 8, 0.6, 8)
     assert abs(((m > 0) == (m2 > 0)).mean() - 0.52) < 0.01
-    # CSR positions: stable by target, loops last per row
+    # CSR positions: by (target, source), equal pairs in input order
     import torch
     ei = torch.tensor([[1, 2, 0], [1, 0, 1]])
-    assert csr_positions(ei, 3).tolist() == [2, 0, 3, 1, 4, 5]
+    # edges (src->dst): 1->1, 2->0, 0->1, loops 0->0, 1->1, 2->2
+    # rows: 0: [0->0 (loop), 2->0]; 1: [0->1, 1->1 (input), 1->1 (loop)]; 2: [2->2]
+    assert csr_positions(ei, 3).tolist() == [3, 1, 2, 0, 4, 5]
