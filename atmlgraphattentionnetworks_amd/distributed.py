@@ -181,7 +181,10 @@ def gather_output(local_out: torch.Tensor, bounds: List[int], group=None) -> tor
 # ---------------------------------------------------------------------------
 def _time_steps(step, warmup: int, steps: int, dev) -> float:
     """W untimed steps, then K steps bracketed by barrier + synchronize on both
-    sides; returns the MAX over ranks of the K-step wall time (seconds)."""
+    sides; returns the MAX over ranks of the K-step wall time (seconds).  Each
+    rank's clock runs from just after the opening barrier to its own final
+    synchronize, so a straggler shows up in the max while the closing
+    barrier's latency is not billed as step time."""
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -191,14 +194,15 @@ def _time_steps(step, warmup: int, steps: int, dev) -> float:
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.barrier()
+    # the default group is gloo (bench_distributed): a host tensor
+    t = torch.tensor([elapsed], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def _strong_probe(w, layer, dev, world, rank, exchange, steps, warmup, use_graph):
+def _strong_probe(w, layer, dev, world, rank, exchange, steps, warmup, use_graph, group=None):
     """ONE shared graph of the workload's shape, node-range partitioned across
     the ranks: per step, project own rows -> RCCL all-gather of
     the packed [Wh | s_src] table (exchange="allgather") or full projection on
@@ -209,7 +213,7 @@ def _strong_probe(w, layer, dev, world, rank, exchange, steps, warmup, use_graph
     x, ei = make_inputs(w, dev)  # same seeds on every rank -> the same graph
     csr = get_csr(ei, x.size(0))
     del ei
-    sh = ShardedGAT(layer, csr, world, rank, exchange=exchange)
+    sh = ShardedGAT(layer, csr, world, rank, exchange=exchange, group=group)
     xl = sh.local_x(x)
     launch = "eager"
     g_proj = g_edge = None
@@ -277,7 +281,11 @@ def bench_distributed(args, metric: str):
     sys.stdout.flush()
     saved_stdout = os.dup(1)
     os.dup2(2, 1)
-    dist.init_process_group("nccl", device_id=dev)
+    # The weak-scaling step has no data-path collective, so the default group is
+    # gloo (barriers and the max-over-ranks reduction on the host): no RCCL
+    # proxy threads compete with the launch thread while it is timed.  The RCCL
+    # group is created afterwards, for the strong-scaling probe's all-gather.
+    dist.init_process_group("gloo")
 
     w = WORKLOADS[args.workload]
     torch.manual_seed(0)
@@ -303,7 +311,7 @@ def bench_distributed(args, metric: str):
             step, launch = g.replay, "hipGraph"
         t = _time_steps(step, args.warmup, args.steps, dev)
         ms = t * 1e3 / args.steps
-        e_blk = torch.tensor([csr.num_edges], dtype=torch.float64, device=dev)
+        e_blk = torch.tensor([csr.num_edges], dtype=torch.float64)
         dist.all_reduce(e_blk)
         total_edges = float(e_blk.item())
 
@@ -327,9 +335,11 @@ def bench_distributed(args, metric: str):
 
         strong = []
         if not getattr(args, "no_strong_probe", False):
+            rccl = dist.new_group(backend="nccl")
             for ex in ("allgather", "replicate"):
                 strong.append(_strong_probe(w, layer, dev, world, rank, ex, max(args.steps // 2, 5),
-                                            max(args.warmup // 2, 2), not args.no_graph))
+                                            max(args.warmup // 2, 2), not args.no_graph,
+                                            group=rccl))
 
     from bench import HBM_PEAK_GBS, edge_kernel_bytes, load_traffic  # noqa: E402
     alg = edge_kernel_bytes(n_block, csr.num_edges, w.heads, w.out_channels, w.concat)
