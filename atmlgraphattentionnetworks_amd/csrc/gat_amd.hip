@@ -346,6 +346,145 @@ __device__ __forceinline__ float group_sum16(float v, int w) {
 }
 
 // ---------------------------------------------------------------------------
+// Projection, software-pipelined K loop (Fin > 64).  fp32 MFMA throughput
+// (157 TF) bounds a [N, Fin] x [Fin, 64] projection at large Fin (Reddit:
+// 18 GFLOP -> 115 us).  The K-tiled kernel reads its MFMA A operand straight
+// from global memory, 16 rows x 16 B per load instruction, so every x cache
+// line passes through L1 eight times.  Here:
+//   * block = 128 rows x BN (<= 64) columns; wave w owns rows [32w, 32w+32)
+//     as two 16-row groups, so every W fragment read from LDS feeds two MFMAs;
+//   * per 64-wide K chunk, x [128 x 64] and W [BN x 64] are staged through
+//     LDS with fully coalesced loads (64 lanes = one 256-B row chunk) and the
+//     A/B fragments read back conflict-free (row strides 68 and 66);
+//   * chunk c+1's x and W loads are in flight in registers while chunk c's
+//     16 k-steps x 8 MFMAs run; two barriers per chunk.
+// Epilogue: bias, Wh store, score dot products by shuffles within F lanes.
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void k_project_pipe(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
+    float* __restrict__ s_dst) {
+    constexpr int BK = 64, KS = BK / 4, BN = NT * 16, BM = 128;
+    constexpr int WL = BN * BK / 256;  // W-tile elements per thread
+    constexpr int XL = BM * BK / 256;  // x-tile elements per thread (32)
+    constexpr int WS = BK + 2, XS = BK + 4;
+    __shared__ float wsm[BN * WS];
+    __shared__ float xsm[BM * XS];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int blk0 = blockIdx.x * BM;
+    const int row0 = blk0 + w * 32;
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    float xn[XL], wn[WL];
+    auto load_chunk = [&](int k0) {
+        // x: element idx = tid + 256 q -> row idx / 64, k idx % 64: one wave
+        // instruction reads one row's 64 consecutive k (coalesced)
+        // Raw loads only (no math on the loaded values until the LDS write, so
+        // nothing forces a wait between them).  Clamped addresses keep every
+        // load in bounds: x rows >= n feed output rows that are never stored,
+        // and k >= fin is zeroed on the W side at the LDS write, so x needs no
+        // mask.  32-bit element offsets (n * fin < 2^31, checked at launch).
+        const unsigned kc = (unsigned)min(k0 + (tid & 63), fin - 1);
+#pragma unroll
+        for (int q = 0; q < XL; ++q) {
+            const int r = min(blk0 + (tid >> 6) + 4 * q, n - 1);
+            xn[q] = X[(unsigned)r * (unsigned)fin + kc];
+        }
+#pragma unroll
+        for (int q = 0; q < WL; ++q) {
+            const int idx = tid + q * 256;
+            const int nn = min(idx / BK, HF - 1), gk = min(k0 + idx % BK, fin - 1);
+            wn[q] = W[(unsigned)nn * (unsigned)fin + (unsigned)gk];
+        }
+    };
+    load_chunk(0);
+    for (int k0 = 0; k0 < fin; k0 += BK) {
+        __syncthreads();  // the previous chunk's fragment reads are done
+#pragma unroll
+        for (int q = 0; q < XL; ++q) xsm[((tid >> 6) + 4 * q) * XS + (tid & 63)] = xn[q];
+#pragma unroll
+        for (int q = 0; q < WL; ++q) {
+            const int idx = tid + q * 256;
+            const bool ok = idx / BK < HF && k0 + idx % BK < fin;
+            wsm[(idx / BK) * WS + idx % BK] = ok ? wn[q] : 0.f;
+        }
+        __syncthreads();
+        if (k0 + BK < fin) load_chunk(k0 + BK);  // in flight during this chunk's MFMAs
+        const int ksteps = min(KS, (fin - k0 + 3) / 4);
+        const float* xa0 = xsm + (w * 32 + cl) * XS + kq;
+        const float* xa1 = xa0 + 16 * XS;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            if (s < ksteps) {  // block-uniform
+                const float a0 = xa0[4 * s], a1v = xa1[4 * s];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const float b = wsm[(t * 16 + cl) * WS + 4 * s + kq];
+                    acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][t], 0, 0, 0);
+                    acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v, b, acc[1][t], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    const int hfp = round_up4(HF);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        const int rbase = row0 + 16 * g + (lane >> 4) * 4;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int cc = t * 16 + cl;
+            const float bb = cc < HF ? bW[cc] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = acc[g][t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
+                acc[g][t][i] = v;
+                const int rr = rbase + i;
+                if (rr < n && cc < hfp) Wh[(size_t)rr * ld_wh + cc] = v;
+            }
+        }
+        // scores: head = F consecutive lanes of one 16-column tile (F | 16)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int cc = t * 16 + cl;
+            const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
+            float p1[4], p2[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                p1[i] = acc[g][t][i] * w1;
+                p2[i] = acc[g][t][i] * w2;
+            }
+            for (int off = 1; off < F; off <<= 1)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    p1[i] += __shfl_xor(p1[i], off);
+                    p2[i] += __shfl_xor(p2[i], off);
+                }
+            const int h = cc / F;
+            if ((cl & (F - 1)) == 0 && h < H) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = rbase + i;
+                    if (rr >= n) continue;
+                    Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
+                    s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Projection, direct-load variant (F a power of two): one wave owns 16 node
 // rows x TW column tiles (TW*16 columns, whole heads), so a PPI-shape layer
 // runs 2x the waves of the LDS-tiled kernel.  MFMA A/B fragments are loaded
@@ -1846,7 +1985,10 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     const size_t wk_out = (size_t)64 * (nt * 16 + 4) * sizeof(float);
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) |
                              reinterpret_cast<uintptr_t>(wh)) & 15) == 0;
-    const bool wk_ok = fin > 0 && fin <= 64 && aligned16 &&
+    int wk_max = 64;  // GAT_PROJ_WK_MAX (A/B knob): largest fin for the whole-K kernel
+    if (const char* v = std::getenv("GAT_PROJ_WK_MAX")) wk_max = std::atoi(v);
+    const bool wk_ok = fin > 0 && fin <= wk_max && aligned16 &&
+                       (wk_lds > wk_out ? wk_lds : wk_out) <= 160 * 1024 &&
                        (pk == nullptr || std::strcmp(pk, "wk") == 0);
     if (wk_ok) {
         const size_t lds = wk_lds > wk_out ? wk_lds : wk_out;
@@ -1863,6 +2005,25 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
             default: return GAT_EUNSUPPORTED;
         }
 #undef GAT_WK_CASE
+        return status_of(hipGetLastError());
+    }
+    // pipelined K loop for large fin (F a power of two dividing 16, HF <= 64);
+    // GAT_PROJ_KERNEL=tiled keeps the K-tiled kernel (A/B knob)
+    const bool pipe_ok = fin > 64 && nt <= 4 && pow2_f && f <= 16 &&
+                         (long long)n * fin < (1LL << 31) &&
+                         (pk == nullptr || std::strcmp(pk, "pipe") == 0);
+    if (pipe_ok) {
+        const dim3 gp((n + 127) / 128), bp(256);
+#define GAT_PIPE_CASE(NT)                                                                     \
+    case NT:                                                                                  \
+        hipLaunchKernelGGL((k_project_pipe<NT>), gp, bp, 0, st, x, n, fin, w, b, a_src, c_src, \
+                           a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst);        \
+        break;
+        switch (nt) {
+            GAT_PIPE_CASE(1) GAT_PIPE_CASE(2) GAT_PIPE_CASE(3) GAT_PIPE_CASE(4)
+            default: return GAT_EUNSUPPORTED;
+        }
+#undef GAT_PIPE_CASE
         return status_of(hipGetLastError());
     }
     if (pow2_f && pk != nullptr && std::strcmp(pk, "direct") == 0) {
