@@ -610,6 +610,19 @@ __global__ __launch_bounds__(256) void k_project_direct(
 // leave as coalesced float4 stores and each (row, head) score is one short
 // dot product per thread.  Two barriers per workgroup, no K loop.
 // ---------------------------------------------------------------------------
+// LDS layout of k_project_wk: [X tile | W tile] (reused for the output tile
+// after the MFMAs), then the epilogue parameters [b | a1 | a2 (BN each) |
+// c1 | c2 (64 each)] from this offset (floats).
+__host__ __device__ inline int wk_param_offset(int fin, int nt) {
+    const int tiles = ((64 * fin + 3) & ~3) + nt * 16 * fin;
+    const int out = 64 * (nt * 16 + 4);
+    return ((tiles > out ? tiles : out) + 3) & ~3;
+}
+
+__host__ __device__ inline int wk_lds_floats(int fin, int nt) {
+    return wk_param_offset(fin, nt) + 3 * nt * 16 + 128;
+}
+
 template <int NT>
 __global__ __launch_bounds__(256) void k_project_wk(
     const float* __restrict__ X, int n, int fin,
@@ -628,6 +641,27 @@ __global__ __launch_bounds__(256) void k_project_wk(
     const int xs_n = round_up4(BM * fin);  // X tile floats (16-B aligned W tile after it)
     float* Xs = smem;
     float* Ws = smem + xs_n;
+    // epilogue parameters in their own LDS region (past the X/W tiles and the
+    // output tile): loaded now, with the tiles, instead of after the MFMAs
+    float* Ps = smem + wk_param_offset(fin, NT);
+    float* bs = Ps;
+    float* a1s = Ps + BN;
+    float* a2s = Ps + 2 * BN;
+    float* c1s = Ps + 3 * BN;
+    float* c2s = c1s + 64;
+    if (tid < BN) {
+        const bool ok = tid < HF;
+        const int cc = ok ? tid : 0;
+        const float bv = bW[cc], av1 = a1[cc], av2 = a2[cc];
+        bs[tid] = ok ? bv : 0.f;
+        a1s[tid] = ok ? av1 : 0.f;
+        a2s[tid] = ok ? av2 : 0.f;
+    }
+    if (tid < H) {
+        const float v1 = c1[tid], v2 = c2[tid];
+        c1s[tid] = v1;
+        c2s[tid] = v2;
+    }
 
     // X rows [row0, row0+rows) are one contiguous chunk (row0*fin*4 = 256*b*fin bytes:
     // 16-B aligned) and W [HF, fin] another.  Each thread issues ALL its float4
@@ -702,7 +736,7 @@ __global__ __launch_bounds__(256) void k_project_wk(
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const int cc = t * 16 + cl;
-        const float bb = cc < HF ? bW[cc] : 0.f;  // Linear bias inside Wh (GAT.py:43)
+        const float bb = bs[cc];  // Linear bias inside Wh (GAT.py:43); 0 past HF
 #pragma unroll
         for (int i = 0; i < 4; ++i) Os[(w * 16 + kq * 4 + i) * OS + cc] = acc[t][i] + bb;
     }
@@ -723,13 +757,15 @@ __global__ __launch_bounds__(256) void k_project_wk(
     for (int idx = tid; idx < rows * H; idx += 256) {
         const int r = idx / H, h = idx - r * H;
         const float* o = Os + r * OS + h * F;
+        const float* p1 = a1s + h * F;
+        const float* p2 = a2s + h * F;
         float v1 = 0.f, v2 = 0.f;
         for (int f = 0; f < F; ++f) {
-            v1 = fmaf(o[f], a1[h * F + f], v1);
-            v2 = fmaf(o[f], a2[h * F + f], v2);
+            v1 = fmaf(o[f], p1[f], v1);
+            v2 = fmaf(o[f], p2[f], v2);
         }
-        Ss[(size_t)(row0 + r) * ld_s + h] = v1 + c1[h];
-        s_dst[(size_t)(row0 + r) * H + h] = v2 + c2[h];
+        Ss[(size_t)(row0 + r) * ld_s + h] = v1 + c1s[h];
+        s_dst[(size_t)(row0 + r) * H + h] = v2 + c2s[h];
     }
 }
 
@@ -1981,8 +2017,8 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     // (K-tiled, LDS epilogue), "direct" (register-direct, F a power of two)
     const char* pk = std::getenv("GAT_PROJ_KERNEL");
     const bool pow2_f = next_pow2(f) == f;
-    const size_t wk_lds = (size_t)(round_up4(64 * fin) + nt * 16 * fin) * sizeof(float);
-    const size_t wk_out = (size_t)64 * (nt * 16 + 4) * sizeof(float);
+    const size_t wk_lds = (size_t)wk_lds_floats(fin, nt) * sizeof(float);
+    const size_t wk_out = 0;  // the output tile is inside wk_lds_floats
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) |
                              reinterpret_cast<uintptr_t>(wh)) & 15) == 0;
     int wk_max = 64;  // GAT_PROJ_WK_MAX (A/B knob): largest fin for the whole-K kernel
