@@ -335,11 +335,23 @@ def bench_distributed(args, metric: str):
 
         strong = []
         if not getattr(args, "no_strong_probe", False):
-            rccl = dist.new_group(backend="nccl")
-            for ex in ("allgather", "replicate"):
-                strong.append(_strong_probe(w, layer, dev, world, rank, ex, max(args.steps // 2, 5),
-                                            max(args.warmup // 2, 2), not args.no_graph,
-                                            group=rccl))
+            # evidence only (the reported value is the weak-scaling line): a failure
+            # here is recorded in the JSON instead of costing the line
+            try:
+                rccl = dist.new_group(backend="nccl")
+            except Exception as exc:  # noqa: BLE001
+                rccl = None
+                strong.append({"error": f"RCCL group: {type(exc).__name__}: {exc}"[:300]})
+            if rccl is not None:
+                for ex in ("allgather", "replicate"):
+                    try:
+                        strong.append(_strong_probe(w, layer, dev, world, rank, ex,
+                                                    max(args.steps // 2, 5),
+                                                    max(args.warmup // 2, 2), not args.no_graph,
+                                                    group=rccl))
+                    except Exception as exc:  # noqa: BLE001
+                        strong.append({"exchange": ex,
+                                       "error": f"{type(exc).__name__}: {exc}"[:300]})
 
     from bench import HBM_PEAK_GBS, edge_kernel_bytes, load_traffic  # noqa: E402
     alg = edge_kernel_bytes(n_block, csr.num_edges, w.heads, w.out_channels, w.concat)
