@@ -2131,7 +2131,10 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
     // V float4s per lane (one head per lane needs f % 4V == 0): fewer, fuller
     // waves; GAT_EDGE_V overrides
     const bool dropping = drop.thresh != 0u;
-    int vv = 1;
+    // long rows (Reddit scale) take two float4s per lane: half the lanes per row,
+    // twice the rows per wave (tools/tune_edge.py: Reddit 3.34 -> 3.23 ms; PPI and
+    // arxiv are no faster with V = 2)
+    int vv = edges_per_row_hint >= 128 ? 2 : 1;
     if (const char* ev = std::getenv("GAT_EDGE_V")) vv = std::atoi(ev);
     if (vv != 1 && vv != 2 && vv != 4) vv = 1;
     if (dropping) vv = 1;  // the dropout variant is instantiated for V = 1, U = 8 only
@@ -2147,7 +2150,8 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
     if (grp_ok && (s_src == nullptr || kernel_choice("GAT_EDGE_KERNEL", "group", "generic"))) {
         // edges per chunk: short rows want short chunks (less padding), long rows
         // more loads in flight; GAT_EDGE_U overrides
-        int u = edges_per_row_hint <= 0 ? 8 : edges_per_row_hint <= 12 ? 4
+        // (tools/tune_edge.py: PPI, ~28 per row, 36.9 us at U = 8 -> 33.1 us at U = 4)
+        int u = edges_per_row_hint <= 0 ? 8 : edges_per_row_hint <= 32 ? 4
               : edges_per_row_hint <= 64 ? 8 : 16;
         if (const char* eu = std::getenv("GAT_EDGE_U")) u = std::atoi(eu);
         if (dropping) u = 8;
