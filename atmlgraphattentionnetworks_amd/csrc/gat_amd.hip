@@ -2045,9 +2045,9 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     }
     // pipelined K loop for large fin (F a power of two dividing 16, HF <= 64);
     // GAT_PROJ_KERNEL=tiled keeps the K-tiled kernel (A/B knob)
-    const bool pipe_ok = fin > 64 && nt <= 4 && pow2_f && f <= 16 &&
-                         (long long)n * fin < (1LL << 31) &&
-                         (pk == nullptr || std::strcmp(pk, "pipe") == 0);
+    const bool force_pipe = pk != nullptr && std::strcmp(pk, "pipe") == 0;
+    const bool pipe_ok = (fin > 64 || force_pipe) && fin > 0 && nt <= 4 && pow2_f && f <= 16 &&
+                         (long long)n * fin < (1LL << 31) && (pk == nullptr || force_pipe);
     if (pipe_ok) {
         const dim3 gp((n + 127) / 128), bp(256);
 #define GAT_PIPE_CASE(NT)                                                                     \

@@ -274,6 +274,8 @@ def bench_distributed(args, metric: str):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if os.environ.get("GAT_BENCH_SHARE_GPU0"):  # testing on a one-GPU box: every rank on cuda:0
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     # rank 0 prints exactly one JSON line on stdout; RCCL prints its banner and

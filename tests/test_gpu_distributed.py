@@ -44,3 +44,30 @@ def test_sharded_hip_path_matches_single_gpu(P, exchange, concat):
     full = torch.cat(outs).cpu()
     ref = gat_layer_forward_from_state(state, x.cpu(), ei.cpu(), H, concat)
     torch.testing.assert_close(full, ref, atol=1e-5, rtol=1e-5)
+
+
+def test_bench_weak_scaling_two_ranks_one_line(tmp_path):
+    """bench.py's multi-GPU path end to end with 2 torchrun ranks sharing cuda:0
+    (GAT_BENCH_SHARE_GPU0; the pool's boxes have one GPU): gloo barriers, the
+    max-over-ranks timing, and exactly one JSON line on rank 0's stdout.  The
+    RCCL strong-scaling probe needs distinct GPUs and is skipped here."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, GAT_BENCH_SHARE_GPU0="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--no-strong-probe", "--steps", "10", "--warmup", "3"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
+    assert d["steps"] == 10 and d["unit"] == "edges/s"
