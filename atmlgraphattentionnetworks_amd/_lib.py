@@ -45,24 +45,25 @@ SIGNATURES = {
     "gat_edge_aggregate_ex": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
                                        _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
                                        _c_int, _c_int, _c_float, _c_float, _c_u64, _c_vp, _c_vp,
-                                       _c_vp, _c_vp, _c_int, _c_vp]),
+                                       _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
+    "gat_dropout_seed_next": (_c_int, [_c_vp, _c_vp, _c_vp]),
     "gat_csc_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csc_build": (_c_int, [_c_vp, _c_vp, _c_int, _c_ll, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                ctypes.c_size_t, _c_vp]),
     "gat_bwd_table_layout": (_c_int, [_c_int, _c_int, _c_int, _c_int_p]),
     "gat_bwd_targets": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp,
                                  _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
-                                 _c_float, _c_float, _c_u64, _c_vp, _c_vp, _c_int, _c_int,
+                                 _c_float, _c_float, _c_u64, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
                                  _c_vp]),
     "gat_bwd_sources_parts": (_c_int, [_c_int, _c_int, _c_int, _c_int_p]),
     "gat_bwd_sources": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int,
                                  _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_float,
-                                 _c_float, _c_u64, _c_vp, _c_int, _c_vp, _c_int, _c_int,
+                                 _c_float, _c_u64, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_int,
                                  _c_vp]),
     "gat_edge_backward_rows": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp,
                                         _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                                         _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_int, _c_float,
-                                        _c_float, _c_u64, _c_vp, _c_vp, _c_int, _c_vp]),
+                                        _c_float, _c_u64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_weight_grad_workspace_size": (_c_int, [_c_int, _c_int, _c_int, _c_size_p]),
     "gat_weight_grad": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_int, _c_int, _c_vp, _c_vp,
                                  ctypes.c_size_t, _c_vp]),

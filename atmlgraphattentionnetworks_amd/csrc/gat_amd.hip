@@ -100,7 +100,19 @@ struct DropArgs {
     unsigned thresh;   // 0: no dropout
     float scale;       // 1 / (1 - p)
     unsigned seed_lo, seed_hi;
+    const unsigned long long* seed_ptr;  // if set, the seed is read from device memory
 };
+
+// The seed may live in device memory (gat_dropout_seed_next), so that a
+// captured HIP graph draws a fresh mask on every replay.
+__device__ __forceinline__ DropArgs resolve_drop(DropArgs d) {
+    if (d.seed_ptr != nullptr) {
+        const unsigned long long sv = *d.seed_ptr;
+        d.seed_lo = (unsigned)sv;
+        d.seed_hi = (unsigned)(sv >> 32);
+    }
+    return d;
+}
 
 __host__ __device__ __forceinline__ unsigned mix32(unsigned x) {
     x ^= x >> 16;
@@ -119,8 +131,10 @@ __device__ __forceinline__ float drop_factor(const DropArgs& d, long long k, int
     return mix32(a ^ b) >= d.thresh ? d.scale : 0.f;
 }
 
-DropArgs make_drop(float p, unsigned long long seed) {
+DropArgs make_drop(float p, unsigned long long seed,
+                   const unsigned long long* seed_dev = nullptr) {
     DropArgs d;
+    d.seed_ptr = seed_dev;
     double t = std::floor((double)p * 4294967296.0 + 0.5);
     if (t < 0.0) t = 0.0;
     if (t > 4294967295.0) t = 4294967295.0;
@@ -790,8 +804,9 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
     const float* __restrict__ s_dst,
     int H, int F, int HF, int concat, int act, float slope, const float* __restrict__ bias,
-    float* __restrict__ out, int ld_out, float* __restrict__ lse, DropArgs drop,
+    float* __restrict__ out, int ld_out, float* __restrict__ lse, DropArgs drop_arg,
     float* __restrict__ y_heads) {
+    const DropArgs drop = resolve_drop(drop_arg);
     constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;  // edges per chunk
     constexpr int R = C * HP / kWave;                          // score slots per lane
     constexpr int EPI = kWave / LPE;                           // edges per gather step
@@ -959,7 +974,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const float* __restrict__ a_src, const float* __restrict__ c_src,
     const float* __restrict__ s_dst, int H, int F, int HF, int concat, float slope,
     const float* __restrict__ bias, float* __restrict__ out, int ld_out,
-    float* __restrict__ lse, DropArgs drop, float* __restrict__ y_heads) {
+    float* __restrict__ lse, DropArgs drop_arg, float* __restrict__ y_heads) {
+    const DropArgs drop = resolve_drop(drop_arg);
     constexpr int CL = (U + G - 1) / G;  // col values held per lane per chunk
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
@@ -1273,8 +1289,9 @@ __global__ __launch_bounds__(64) void k_edge_bwd_rows(
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
     const float* __restrict__ s_dst, const float* __restrict__ lse,
     const float* __restrict__ y_heads, const float* __restrict__ g, int H, int F, int HF,
-    int concat, int act, float slope, DropArgs drop, float* __restrict__ ds_dst,
+    int concat, int act, float slope, DropArgs drop_arg, float* __restrict__ ds_dst,
     float2* __restrict__ az_out) {
+    const DropArgs drop = resolve_drop(drop_arg);
     constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;
     constexpr int R = C * HP / kWave;
     __shared__ float dy_s[GAT_MAX_HF];
@@ -1364,8 +1381,9 @@ __global__ __launch_bounds__(256) void k_edge_bwd_grp(
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ a_src,
     const float* __restrict__ c_src, const float* __restrict__ s_dst,
     const float* __restrict__ lse, const float* __restrict__ y_heads,
-    const float* __restrict__ g, int H, int F, int HF, int concat, float slope, DropArgs drop,
+    const float* __restrict__ g, int H, int F, int HF, int concat, float slope, DropArgs drop_arg,
     float* __restrict__ ds_dst, float2* __restrict__ az_out) {
+    const DropArgs drop = resolve_drop(drop_arg);
     constexpr int CL = (U + G - 1) / G;
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
@@ -1473,8 +1491,9 @@ __global__ __launch_bounds__(256) void k_bwd_targets(
     const float* __restrict__ a_src, const float* __restrict__ c_src,
     const float* __restrict__ s_dst, const float* __restrict__ lse,
     const float* __restrict__ y_heads, const float* __restrict__ g, int H, int F, int HF,
-    int concat, float slope, DropArgs drop, float* __restrict__ ds_dst,
+    int concat, float slope, DropArgs drop_arg, float* __restrict__ ds_dst,
     float* __restrict__ T, int ld_t) {
+    const DropArgs drop = resolve_drop(drop_arg);
     constexpr int CL = (U + G - 1) / G;
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
@@ -1571,7 +1590,8 @@ __global__ __launch_bounds__(256) void k_bwd_sources(
     const float* __restrict__ T, int ld_t, const float* __restrict__ ds_dst,
     const float* __restrict__ a_src, const float* __restrict__ c_src,
     const float* __restrict__ a_dst, int H, int F, int HF, int concat, float slope,
-    DropArgs drop, float* __restrict__ dwh, int ld_dwh, float* __restrict__ part) {
+    DropArgs drop_arg, float* __restrict__ dwh, int ld_dwh, float* __restrict__ part) {
+    const DropArgs drop = resolve_drop(drop_arg);
     constexpr int CL = (U + G - 1) / G;
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
@@ -1931,6 +1951,18 @@ int wgrad_chunks(int n, int fin, int hf) {
     return c < 1 ? 1 : c;
 }
 
+// counter -> seed: splitmix64 of the counter value, then counter += 1
+__global__ void k_seed_next(unsigned long long* __restrict__ counter,
+                            unsigned long long* __restrict__ seed_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const unsigned long long v = counter[0];
+    counter[0] = v + 1ull;
+    unsigned long long z = v + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    seed_out[0] = z ^ (z >> 31);
+}
+
 constexpr size_t kAlign = 256;
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
@@ -2246,12 +2278,13 @@ int gat_edge_aggregate_ex(const int* rowptr, const int* col, const int* row_orde
                           int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
                           const float* a_src, const float* c_src, const float* s_dst, int heads,
                           int f, int concat, int score_act, float act_param, float dropout_p,
-                          unsigned long long seed, const float* bias, float* out, float* lse,
-                          float* y_heads, int edges_per_row_hint, void* stream) {
+                          unsigned long long seed, const unsigned long long* seed_dev,
+                          const float* bias, float* out, float* lse, float* y_heads,
+                          int edges_per_row_hint, void* stream) {
     if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
     return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src,
                                ld_s, a_src, c_src, s_dst, heads, f, concat, score_act, act_param,
-                               bias, out, lse, y_heads, make_drop(dropout_p, seed),
+                               bias, out, lse, y_heads, make_drop(dropout_p, seed, seed_dev),
                                edges_per_row_hint, stream);
 }
 
@@ -2261,6 +2294,13 @@ size_t csr_key_sort_tmp_bytes(long long nnz, int n) {
     const unsigned kb = key_bits(n);
     const hipError_t e = rocprim::radix_sort_keys(nullptr, tmp, k, k, (size_t)nnz, 0u, 2 * kb);
     return e == hipSuccess ? tmp : 0;
+}
+
+int gat_dropout_seed_next(unsigned long long* counter, unsigned long long* seed_out,
+                          void* stream) {
+    if (counter == nullptr || seed_out == nullptr) return GAT_EINVAL;
+    hipLaunchKernelGGL(k_seed_next, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, seed_out);
+    return status_of(hipGetLastError());
 }
 
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes) {
@@ -2390,8 +2430,8 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
                     const float* c_src, const float* s_dst, const float* lse,
                     const float* y_heads, const float* grad_out, int heads, int f, int concat,
                     float negative_slope, float dropout_p, unsigned long long seed,
-                    float* ds_dst, float* table, int ld_t, int edges_per_row_hint,
-                    void* stream) {
+                    const unsigned long long* seed_dev, float* ds_dst, float* table, int ld_t,
+                    int edges_per_row_hint, void* stream) {
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
     int need_ld = 0;
@@ -2401,7 +2441,7 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
     const int rows = row_end - row_begin;
     if (rows == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
-    const DropArgs drop = make_drop(dropout_p, seed);
+    const DropArgs drop = make_drop(dropout_p, seed, seed_dev);
     const int hf = heads * f;
     const int g = next_pow2(hf / 4);
     const int u = edges_per_row_hint > 0 && edges_per_row_hint <= 12 ? 4 : 8;
@@ -2442,8 +2482,9 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
                     const float* wh, int ld_wh, const float* table, int ld_t,
                     const float* ds_dst, const float* a_src, const float* c_src,
                     const float* a_dst, int heads, int f, int concat, float negative_slope,
-                    float dropout_p, unsigned long long seed, float* dwh, int ld_dwh,
-                    float* partials, int num_parts, int edges_per_row_hint, void* stream) {
+                    float dropout_p, unsigned long long seed, const unsigned long long* seed_dev,
+                    float* dwh, int ld_dwh, float* partials, int num_parts,
+                    int edges_per_row_hint, void* stream) {
     if (heads <= 0 || f <= 0 || num_nodes < 0 || num_parts <= 0 || (num_parts & 3))
         return GAT_EINVAL;
     if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
@@ -2452,7 +2493,7 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
     if (!bwd_recompute_ok(heads, f, negative_slope, wh, ld_wh)) return GAT_EUNSUPPORTED;
     if (dropout_p > 0.f && csc_eid == nullptr) return GAT_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    const DropArgs drop = make_drop(dropout_p, seed);
+    const DropArgs drop = make_drop(dropout_p, seed, seed_dev);
     const int g = next_pow2(hf / 4);
     int u = edges_per_row_hint > 0 && edges_per_row_hint <= 12 ? 4 : 8;
     if (const char* v = std::getenv("GAT_BWD_U")) u = std::atoi(v) == 4 ? 4 : 8;  // A/B knob
@@ -2481,8 +2522,8 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
                            const float* c_src, const float* s_dst, const float* lse,
                            const float* y_heads, const float* grad_out, int heads, int f,
                            int concat, int score_act, float act_param, float dropout_p,
-                           unsigned long long seed, float* ds_dst, float* az_csc,
-                           int edges_per_row_hint, void* stream) {
+                           unsigned long long seed, const unsigned long long* seed_dev,
+                           float* ds_dst, float* az_csc, int edges_per_row_hint, void* stream) {
     if (score_act < GAT_ACT_LEAKY_RELU || score_act > GAT_ACT_HEAD_SOFTMAX) return GAT_EINVAL;
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
     const int hf = heads * f;
@@ -2492,7 +2533,7 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
     const int rows = row_end - row_begin;
     if (rows == 0) return GAT_OK;
     hipStream_t st = (hipStream_t)stream;
-    const DropArgs drop = make_drop(dropout_p, seed);
+    const DropArgs drop = make_drop(dropout_p, seed, seed_dev);
     float2* az = reinterpret_cast<float2*>(az_csc);
     const int hl = f / 4;
     const bool grp_ok = score_act == GAT_ACT_LEAKY_RELU && act_param >= 0.f && act_param <= 1.f &&

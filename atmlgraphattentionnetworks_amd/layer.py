@@ -321,9 +321,9 @@ class GraphAttentionLayer(torch.nn.Module):
         default_act = act == _lib.GAT_ACT_LEAKY_RELU and 0.0 <= act_param <= 1.0
         if needs_grad or p > 0.0 or not default_act:
             # training path (training.py): dropout of GAT.py:61 and the HIP backward
-            from .training import gat_train_forward, new_dropout_seed
-            seed = new_dropout_seed() if p > 0.0 else 0
-            return gat_train_forward(self, x, csr, p, seed, act, act_param)
+            from .training import gat_train_forward, next_seed_slot
+            slot = next_seed_slot(self, x.device) if p > 0.0 else None
+            return gat_train_forward(self, x, csr, p, 0, act, act_param, seed_slot=slot)
         return gat_forward(x, csr, self.packed(), self.bias.detach(), self.num_heads,
                            self.output_channels, self.concat, act_param)
 

@@ -33,7 +33,7 @@ import torch
 from . import _lib
 from .graph import CSRGraph, get_csc
 
-__all__ = ["GATFunction", "gat_train_forward", "new_dropout_seed"]
+__all__ = ["GATFunction", "gat_train_forward", "new_dropout_seed", "next_seed_slot"]
 
 # rows of per-wave partials written by gat_src_backward
 _MAX_PARTS = 8192
@@ -45,6 +45,27 @@ def new_dropout_seed() -> int:
     return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
 
 
+def next_seed_slot(owner, device: torch.device) -> torch.Tensor:
+    """A device int64[1] holding this call's dropout seed, written on the
+    current stream by ``gat_dropout_seed_next`` from a per-owner device counter
+    (started from torch's default generator, so ``torch.manual_seed`` fixes the
+    sequence).  Because the seed is produced on the GPU, a training step
+    captured in a HIP graph draws a fresh mask on every replay.  The counter is
+    a plain attribute, not a buffer: the state_dict keys stay the reference's."""
+    if device.index is None:
+        device = torch.device(device.type, torch.cuda.current_device())
+    counters = owner.__dict__.setdefault("_dropout_counters", {})
+    ctr = counters.get(device)
+    if ctr is None:
+        ctr = torch.tensor([new_dropout_seed()], dtype=torch.int64, device=device)
+        counters[device] = ctr
+    slot = torch.empty(1, dtype=torch.int64, device=device)
+    _lib.check(_lib.load().gat_dropout_seed_next(
+        ctr.data_ptr(), slot.data_ptr(), torch._C._cuda_getCurrentRawStream(device.index)),
+        "gat_dropout_seed_next")
+    return slot
+
+
 class GATFunction(torch.autograd.Function):
     """Layer forward (training) and backward on prepared inputs.
 
@@ -53,8 +74,9 @@ class GATFunction(torch.autograd.Function):
     they are views of (``GraphAttentionLayer._bind_packed``)."""
 
     @staticmethod
-    def forward(ctx, x, bias, cfg, csr: CSRGraph, pp, *params):
+    def forward(ctx, x, bias, cfg, csr: CSRGraph, pp, seed_slot, *params):
         heads, f, concat, act, act_param, p, seed = cfg
+        p_seed = 0 if seed_slot is None else seed_slot.data_ptr()
         lib = _lib.load()
         n, fin = x.shape
         hf = heads * f
@@ -81,12 +103,12 @@ class GATFunction(torch.autograd.Function):
             csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
             0, n, wh.data_ptr(), hfp, s_src.data_ptr(), heads, pp.a_src.data_ptr(),
             pp.c_src.data_ptr(), s_dst.data_ptr(), heads, f, int(concat), act, act_param, p,
-            seed, bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(),
+            seed, p_seed, bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(),
             csr.num_edges // max(n, 1), stream)
         if rc:
             _lib.check(rc, "gat_edge_aggregate_ex")
         ctx.save_for_backward(x, ws)
-        ctx.csr, ctx.pp, ctx.cfg = csr, pp, cfg
+        ctx.csr, ctx.pp, ctx.cfg, ctx.seed_slot = csr, pp, cfg, seed_slot
         return out
 
     @staticmethod
@@ -126,7 +148,11 @@ class GATFunction(torch.autograd.Function):
             grads[3 * H:4 * H] = ps[2 * hf:2 * hf + H].view(H, 1).unbind(0)
             grads[4 * H:5 * H] = ps[hf:2 * hf].view(H, 1, f).unbind(0)
             grads[5 * H:6 * H] = ps[2 * hf + H:2 * hf + 2 * H].view(H, 1).unbind(0)
-        return (dx, dbias, None, None, None, *grads)
+        return (dx, dbias, None, None, None, None, *grads)
+
+
+def _seed_ptr(ctx) -> int:
+    return 0 if ctx.seed_slot is None else ctx.seed_slot.data_ptr()
 
 
 def _saved_layout(ctx, ws):
@@ -167,7 +193,8 @@ def _backward_recompute(ctx, g, ws, csc, stream):
     rc = lib.gat_bwd_targets(
         csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(), 0,
         n, p_wh, hfp, pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, p_lse, p_y, g.data_ptr(),
-        heads, f, int(concat), act_param, p, seed, base, base + 4 * o_t, ld_t, hint, stream)
+        heads, f, int(concat), act_param, p, seed, _seed_ptr(ctx), base, base + 4 * o_t, ld_t,
+        hint, stream)
     if rc == _lib.GAT_EUNSUPPORTED:
         return None, None
     if rc:
@@ -175,8 +202,8 @@ def _backward_recompute(ctx, g, ws, csc, stream):
     rc = lib.gat_bwd_sources(
         csc.ptr.data_ptr(), csc.dst.data_ptr(), csc.eid.data_ptr(), n, p_wh, hfp,
         base + 4 * o_t, ld_t, base, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
-        pp.a_dst.data_ptr(), heads, f, int(concat), act_param, p, seed, base + 4 * o_dwh, hf,
-        base + 4 * o_part, parts, hint, stream)
+        pp.a_dst.data_ptr(), heads, f, int(concat), act_param, p, seed, _seed_ptr(ctx),
+        base + 4 * o_dwh, hf, base + 4 * o_part, parts, hint, stream)
     if rc:
         _lib.check(rc, "gat_bwd_sources")
     rc = lib.gat_sum_partials(base + 4 * o_part, parts, pw, base + 4 * o_ps,
@@ -214,7 +241,7 @@ def _backward_stored(ctx, g, ws, csc, stream):
         csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
         0, n, csc.csr_to_csc.data_ptr(), p_wh, hfp, p_ss, heads, pp.a_src.data_ptr(),
         pp.c_src.data_ptr(), p_sd, p_lse, p_y, g.data_ptr(), heads, f, int(concat), act,
-        act_param, p, seed, p_dsd, p_az, nnz // max(n, 1), stream)
+        act_param, p, seed, _seed_ptr(ctx), p_dsd, p_az, nnz // max(n, 1), stream)
     if rc:
         _lib.check(rc, "gat_edge_backward_rows")
     rc = lib.gat_src_backward(
@@ -231,11 +258,12 @@ def _backward_stored(ctx, g, ws, csc, stream):
 
 
 def gat_train_forward(layer, x: torch.Tensor, csr: CSRGraph, p: float, seed: int,
-                      act: int = None, act_param: float = None):
+                      act: int = None, act_param: float = None, seed_slot=None):
+    """``seed_slot`` (a device int64[1], ``next_seed_slot``) overrides ``seed``."""
     from .layer import _param_list
     if act is None:
         act, act_param = layer.score_activation()
     pp = layer.packed()
     cfg = (layer.num_heads, layer.output_channels, bool(layer.concat), int(act),
            float(act_param), float(p), int(seed))
-    return GATFunction.apply(x, layer.bias, cfg, csr, pp, *_param_list(layer))
+    return GATFunction.apply(x, layer.bias, cfg, csr, pp, seed_slot, *_param_list(layer))

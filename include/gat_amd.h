@@ -154,6 +154,9 @@ int gat_csr_build(const long long* edge_index, long long num_edges, int num_node
  *              by 1/(1 - dropout_p); the softmax denominator is not dropped.
  *              The mask is a pure function of (seed, k, h): the backward
  *              regenerates it from the same seed.
+ *   seed_dev   optional device pointer: when set, the seed is read from it at run
+ *              time (gat_dropout_seed_next), so a captured HIP graph draws a
+ *              fresh mask on every replay; `seed` is then ignored.
  *   lse        optional [rows, heads]: log-sum-exp per (row, head)
  *   y_heads    optional [rows, heads*f]: per-head aggregation sum_k A_k Wh[j_k]
  *              (after dropout, before head mean and bias)
@@ -163,8 +166,18 @@ int gat_edge_aggregate_ex(const int* rowptr, const int* col, const int* row_orde
                           int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
                           const float* a_src, const float* c_src, const float* s_dst, int heads,
                           int f, int concat, int score_act, float act_param, float dropout_p,
-                          unsigned long long seed, const float* bias, float* out, float* lse,
-                          float* y_heads, int edges_per_row_hint, void* stream);
+                          unsigned long long seed, const unsigned long long* seed_dev,
+                          const float* bias, float* out, float* lse, float* y_heads,
+                          int edges_per_row_hint, void* stream);
+
+/*
+ * Device-side dropout seeds: *seed_out = splitmix64(*counter); *counter += 1, on
+ * `stream`.  Pass seed_out as `seed_dev` to the forward and to the backward of the
+ * same call.  Inside a captured HIP graph each replay advances the counter, so
+ * every replay draws a new mask.
+ */
+int gat_dropout_seed_next(unsigned long long* counter, unsigned long long* seed_out,
+                          void* stream);
 
 /* Workspace bytes gat_csc_build needs for nnz = E + N CSR entries. */
 int gat_csc_workspace_size(long long nnz, int num_nodes, size_t* bytes);
@@ -206,8 +219,8 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
                     const float* c_src, const float* s_dst, const float* lse,
                     const float* y_heads, const float* grad_out, int heads, int f, int concat,
                     float negative_slope, float dropout_p, unsigned long long seed,
-                    float* ds_dst, float* table, int ld_t, int edges_per_row_hint,
-                    void* stream);
+                    const unsigned long long* seed_dev, float* ds_dst, float* table, int ld_t,
+                    int edges_per_row_hint, void* stream);
 
 /* Number of partial rows gat_bwd_sources writes for this shape (a multiple of 4). */
 int gat_bwd_sources_parts(int num_nodes, int heads, int f, int* num_parts);
@@ -223,8 +236,9 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
                     const float* wh, int ld_wh, const float* table, int ld_t,
                     const float* ds_dst, const float* a_src, const float* c_src,
                     const float* a_dst, int heads, int f, int concat, float negative_slope,
-                    float dropout_p, unsigned long long seed, float* dwh, int ld_dwh,
-                    float* partials, int num_parts, int edges_per_row_hint, void* stream);
+                    float dropout_p, unsigned long long seed, const unsigned long long* seed_dev,
+                    float* dwh, int ld_dwh, float* partials, int num_parts,
+                    int edges_per_row_hint, void* stream);
 
 /*
  * Backward pass 1, per TARGET row (softmax + LeakyReLU + dropout backward).
@@ -246,8 +260,8 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
                            const float* c_src, const float* s_dst, const float* lse,
                            const float* y_heads, const float* grad_out, int heads, int f,
                            int concat, int score_act, float act_param, float dropout_p,
-                           unsigned long long seed, float* ds_dst, float* az_csc,
-                           int edges_per_row_hint, void* stream);
+                           unsigned long long seed, const unsigned long long* seed_dev,
+                           float* ds_dst, float* az_csc, int edges_per_row_hint, void* stream);
 
 /*
  * Backward pass 2, per SOURCE row: message backward plus the score terms.

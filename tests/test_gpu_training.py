@@ -310,3 +310,81 @@ def test_params_are_views_of_packed_buffers_after_to_and_step():
     layer.ws[0].weight = torch.nn.Parameter(torch.zeros(4, 12, device=DEV))
     pp2 = layer.packed()
     assert pp2 is not pp and torch.equal(pp2.w[:4], torch.zeros(4, 12, device=DEV))
+
+
+def _splitmix64(v):
+    m = (1 << 64) - 1
+    z = (v + 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def test_device_seed_equals_integer_seed():
+    """gat_dropout_seed_next: the device-seed path gives bitwise the same output
+    and gradients as the integer-seed path with the seed it produced."""
+    from atmlgraphattentionnetworks_amd.graph import get_csr
+    from atmlgraphattentionnetworks_amd.training import gat_train_forward, next_seed_slot
+    n, e, fin, H, F, concat = CASES[0]
+    layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat, seed=5)
+    eid, xd = ei.to(DEV), x.to(DEV)
+    csr = get_csr(eid, n)
+    gout = torch.randn(n, H * F, device=DEV)
+    dev0 = torch.device("cuda", torch.cuda.current_device())
+    slot = next_seed_slot(layer, dev0)
+    seed = int(slot.item()) & ((1 << 64) - 1)
+    ctr = layer._dropout_counters[dev0]
+    assert seed == _splitmix64(int(ctr.item()) - 1)
+    res = []
+    for kw in ({"seed_slot": slot, "seed": 0}, {"seed_slot": None, "seed": seed}):
+        layer.zero_grad()
+        out = gat_train_forward(layer, xd, csr, 0.5, kw["seed"], seed_slot=kw["seed_slot"])
+        (out * gout).sum().backward()
+        res.append([out.detach().clone()] + [p.grad.clone() for p in layer.parameters()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_training_step_captured_in_a_graph():
+    """A whole training step (forward with dropout, loss, backward) captured with
+    torch.cuda.graph: each replay draws a fresh mask from the device counter and
+    equals an eager step with that seed."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    from atmlgraphattentionnetworks_amd.graph import get_csr
+    from atmlgraphattentionnetworks_amd.training import gat_train_forward
+    torch.manual_seed(0)
+    n, fin, H, F = 300, 16, 4, 8
+    ei = _graph(n, 3000, 2).to(DEV)
+    x = torch.randn(n, fin, device=DEV)
+    gout = torch.randn(n, H * F, device=DEV)
+    layer = GraphAttentionLayer(fin, F, num_heads=H, concat=True, dropout=0.5).to(DEV).train()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):  # warm-up: CSR/CSC builds, the seed counter, allocator pools
+            layer.zero_grad(set_to_none=True)
+            (layer(x, ei) * gout).sum().backward()
+    torch.cuda.current_stream().wait_stream(s)
+    layer.zero_grad(set_to_none=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        static_out = layer(x, ei)
+        (static_out * gout).sum().backward()
+    ctr = layer._dropout_counters[torch.device("cuda", torch.cuda.current_device())]
+    csr = get_csr(ei, n)
+    outs = []
+    for _ in range(2):
+        c = int(ctr.item())
+        g.replay()
+        torch.cuda.synchronize()
+        got = [static_out.clone()] + [p.grad.clone() for p in layer.parameters()]
+        outs.append(got[0])
+        seed = _splitmix64(c)
+        ref_layer = GraphAttentionLayer(fin, F, num_heads=H, concat=True, dropout=0.5).to(DEV)
+        ref_layer.load_state_dict(layer.state_dict())
+        ref_out = gat_train_forward(ref_layer, x, csr, 0.5, seed)
+        (ref_out * gout).sum().backward()
+        want = [ref_out.detach()] + [p.grad for p in ref_layer.parameters()]
+        for a, b in zip(got, want):
+            assert torch.equal(a, b)
+    assert not torch.equal(outs[0], outs[1])  # a fresh mask per replay
