@@ -50,6 +50,9 @@ class TrainConfig:
     logging_frequency: int = 10
     verbose: bool = False
     checkpoint: Optional[str] = None  # default: a file in a fresh temp dir
+    # full-batch node classification only: capture the training step (forward,
+    # loss, backward, Adam) in one HIP graph and replay it per epoch
+    use_graph: bool = False
 
 
 @dataclass
@@ -79,6 +82,44 @@ def _load_checkpoint(model, path):
     model.load_state_dict(torch.load(path, weights_only=True))
 
 
+class _GraphedStep:
+    """The epoch's training step (``run_inductive.py:74-84``: forward, NLL on
+    the training nodes, backward, Adam) captured in one HIP graph.  Same math as
+    the eager step; the training nodes are an index tensor (a boolean mask
+    select has a data-dependent size), Adam is ``capturable``, and dropout
+    masks (torch's for the features, the layer's device-seeded attention
+    dropout) are fresh on every replay.  The warm-up steps it runs before
+    capturing are real epochs."""
+
+    def __init__(self, model, data, optimizer, warmup: int = 3):
+        self.model, self.data, self.opt = model, data, optimizer
+        self.idx = data.train_mask.nonzero().squeeze(1)
+        self.y = data.y.index_select(0, self.idx)
+        self.warmup_out = []
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.warmup_out.append(self._step())
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        optimizer.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.out, self.loss = self._step()
+
+    def _step(self):
+        self.opt.zero_grad(set_to_none=True)
+        out = self.model(self.data)
+        loss = F.nll_loss(out.index_select(0, self.idx), self.y)
+        loss.backward()
+        self.opt.step()
+        return out, loss
+
+    def __call__(self):
+        self.graph.replay()
+        return self.out, self.loss
+
+
 def train_node_classification(model: torch.nn.Module, data, cfg: TrainConfig) -> RunResult:
     """One run of ``run_inductive.py:66-133`` on ``data`` (already on the device)."""
     t0 = time.perf_counter()
@@ -86,22 +127,31 @@ def train_node_classification(model: torch.nn.Module, data, cfg: TrainConfig) ->
     ckpt = _checkpoint_path(cfg)
     saved = False
     optimizer = torch.optim.Adam(model.parameters(), lr=cfg.learning_rate,
-                                 weight_decay=cfg.weight_decay)
+                                 weight_decay=cfg.weight_decay, capturable=cfg.use_graph)
     _log(cfg, "Starting training...")
     epoch, stop_counter = 0, 0
     cur_max, cur_min_loss = 0.0, float("inf")
     stop_training = False
+    graphed, pending = None, []
+    if cfg.use_graph:
+        model.train()
+        graphed = _GraphedStep(model, data, optimizer)
+        pending = list(graphed.warmup_out)
     while not stop_training:
         model.train()
-        optimizer.zero_grad()
-        out = model(data)
+        if graphed is not None:
+            out, loss = pending.pop(0) if pending else graphed()
+        else:
+            optimizer.zero_grad()
+            out = model(data)
+            loss = F.nll_loss(out[data.train_mask], data.y[data.train_mask])
         pred = out.argmax(dim=1)
-        loss = F.nll_loss(out[data.train_mask], data.y[data.train_mask])
         correct = (pred[data.train_mask] == data.y[data.train_mask]).sum()
         res.train_accs.append((correct / data.train_mask.sum()).item())
         res.train_losses.append(loss.item())
-        loss.backward()
-        optimizer.step()
+        if graphed is None:
+            loss.backward()
+            optimizer.step()
         if cfg.use_early_stopping:
             if epoch >= cfg.forced_epochs - 1:
                 model.eval()
@@ -266,13 +316,16 @@ def main(argv=None) -> Dict:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--checkpoint", default=None)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="node tasks: replay the training step as one captured HIP graph")
     a = ap.parse_args(argv)
     device = torch.device("cuda")
     graph_task = a.task == "graph"
     cfg = TrainConfig(use_early_stopping=not a.no_early_stopping, num_epochs=a.max_epochs,
                       forced_epochs=a.forced_epochs or (1 if graph_task else 20),
                       early_stopping_patience=a.patience or (5 if graph_task else 100),
-                      verbose=a.verbose, checkpoint=a.checkpoint)
+                      verbose=a.verbose, checkpoint=a.checkpoint,
+                      use_graph=a.graph and not graph_task)
     if a.task == "node":
         out = _node_runs(lambda fin, c: GATNet("GAT", a.dataset, fin), a.dataset, a.runs, cfg,
                          device, a.seed, a.scale)

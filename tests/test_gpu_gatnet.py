@@ -110,3 +110,27 @@ def test_experiment_models_train(task):
         res = train_node_classification(m.to(DEV), d, TrainConfig(use_early_stopping=False,
                                                                   num_epochs=15))
         assert res.train_losses[-1] < res.train_losses[0]
+
+
+def test_node_classification_loop_with_captured_step():
+    """run.py's graphed training step (forward, loss, backward, Adam replayed as
+    one HIP graph; device-seeded attention dropout): learns like the eager loop
+    and runs the same number of epochs without early stopping."""
+    import time
+    from atmlgraphattentionnetworks_amd.datasets import synthetic_node_dataset
+    from atmlgraphattentionnetworks_amd.gatnet import GATNet
+    from atmlgraphattentionnetworks_amd.run import TrainConfig, train_node_classification
+    d = synthetic_node_dataset("Cora", seed=0).to(DEV)
+    res = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        model = GATNet("GAT", "Cora", d.x.size(1)).to(DEV)
+        t0 = time.perf_counter()
+        r = train_node_classification(model, d, TrainConfig(use_early_stopping=False,
+                                                            num_epochs=150, use_graph=graph))
+        res[graph] = (r, time.perf_counter() - t0)
+    for graph, (r, _) in res.items():
+        assert r.epochs == 150 and len(r.train_losses) == 150
+        assert r.train_losses[-1] < 0.7 * r.train_losses[0], (graph, r.train_losses[::30])
+        assert r.test_acc > 0.5, (graph, r.test_acc)
+    print(f"eager {res[False][1]:.2f}s, graphed {res[True][1]:.2f}s for 150 epochs")
