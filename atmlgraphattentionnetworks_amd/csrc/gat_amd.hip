@@ -966,7 +966,7 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
-template <int G, int U, int V, bool FUSED, bool DROP>
+template <int G, int U, int V, bool FUSED>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -999,6 +999,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     }
     const int e0 = rowptr[r], e1 = rowptr[r + 1];
     const bool kahan = e1 - e0 >= 1024;
+    const bool dropping = drop.thresh != 0u;  // kernel-uniform: a scalar branch
     const float sd = s_dst[(size_t)r * H + h];
     float m = -INFINITY, l = 0.f;  // running max in log2 units
     // rows of >= 1024 edges keep Kahan-compensated running sums (lc, cmp) over
@@ -1073,7 +1074,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
                 l += p;  // the softmax denominator never sees the dropout
                 float pa = p;
-                if constexpr (DROP) pa = p * drop_factor(drop, k + u, h, H);
+                if (dropping) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
                 for (int q = 0; q < V; ++q) acc[q] += pa * v[u][q];
             }
@@ -1090,7 +1091,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
                 ls += p;
                 float pa = p;
-                if constexpr (DROP) pa = p * drop_factor(drop, k + u, h, H);
+                if (dropping) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
                 for (int q = 0; q < V; ++q) cs[q] += pa * v[u][q];
             }
@@ -2162,14 +2163,13 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
                           negative_slope <= 1.f;
     // V float4s per lane (one head per lane needs f % 4V == 0): fewer, fuller
     // waves; GAT_EDGE_V overrides
-    const bool dropping = drop.thresh != 0u;
     // long rows (Reddit scale) take two float4s per lane: half the lanes per row,
     // twice the rows per wave (tools/tune_edge.py: Reddit 3.34 -> 3.23 ms; PPI and
     // arxiv are no faster with V = 2)
     int vv = edges_per_row_hint >= 128 ? 2 : 1;
     if (const char* ev = std::getenv("GAT_EDGE_V")) vv = std::atoi(ev);
     if (vv != 1 && vv != 2 && vv != 4) vv = 1;
-    if (dropping) vv = 1;  // the dropout variant is instantiated for V = 1, U = 8 only
+
     while (vv > 1 && f % (4 * vv) != 0) vv >>= 1;
     const int hl = f / (4 * vv);  // lanes per head
     const bool pow2_hl = (f % (4 * vv) == 0) && next_pow2(hl) == hl;
@@ -2186,7 +2186,6 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
         int u = edges_per_row_hint <= 0 ? 8 : edges_per_row_hint <= 32 ? 4
               : edges_per_row_hint <= 64 ? 8 : 16;
         if (const char* eu = std::getenv("GAT_EDGE_U")) u = std::atoi(eu);
-        if (dropping) u = 8;
         const long long threads = (long long)rows * g;
         const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
 #define GAT_GRP_ARGS                                                                          \
@@ -2195,18 +2194,11 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
         drop, y_heads
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
     if (fused)                                                                        \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, true, false>), GAT_GRP_ARGS);       \
+        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, true>), GAT_GRP_ARGS);              \
     else                                                                              \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false, false>), GAT_GRP_ARGS)
+        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), GAT_GRP_ARGS)
 #define GAT_GRP_U(G, VV)                                                              \
-    if (dropping) {                                                                   \
-        if (VV == 1) {                                                                \
-            if (fused)                                                                \
-                hipLaunchKernelGGL((k_edge_grp<G, 8, 1, true, true>), GAT_GRP_ARGS);  \
-            else                                                                      \
-                hipLaunchKernelGGL((k_edge_grp<G, 8, 1, false, true>), GAT_GRP_ARGS); \
-        }                                                                             \
-    } else if (u == 4) { GAT_GRP_LAUNCH(G, 4, VV); }                                  \
+    if (u == 4) { GAT_GRP_LAUNCH(G, 4, VV); }                                         \
     else if (u == 16) { GAT_GRP_LAUNCH(G, 16, VV); }                                  \
     else { GAT_GRP_LAUNCH(G, 8, VV); }
 #define GAT_GRP_G(VV)                                 \
