@@ -72,3 +72,87 @@ def test_csr_workspace_size():
     assert 4 * 1000 * 4 <= small < big
     with pytest.raises(_lib.GatLibraryError):
         _lib.csr_workspace_size(2**31, 10)
+
+
+def test_training_entry_points_validate_without_gpu():
+    """The training and backward entry points reject bad arguments before any
+    launch (so these calls need no device)."""
+    from atmlgraphattentionnetworks_amd import _lib
+    lib = _lib.load()
+    EINVAL, EUNS, OK = _lib.GAT_EINVAL, _lib.GAT_EUNSUPPORTED, _lib.GAT_OK
+
+    def ex(act=0, p=0.5, rows=(0, 10), ld_wh=8):
+        return lib.gat_edge_aggregate_ex(None, None, None, rows[0], rows[1], None, ld_wh, 1, 2,
+                                         None, None, None, 2, 4, 1, act, 0.2, p, 1, None, None,
+                                         None, None, None, 0, None)
+    assert ex(act=7) == EINVAL  # unknown score activation
+    assert ex(p=1.5) == EINVAL and ex(p=-0.1) == EINVAL  # dropout outside [0, 1]
+    assert ex(ld_wh=4) == EINVAL  # ld_wh < heads * f
+    assert ex(rows=(3, 3)) == OK  # nothing to do
+
+    def rows_bwd(act=0, p=0.0, heads=2, f=4):
+        return lib.gat_edge_backward_rows(None, None, None, 0, 10, None, None, 8, None, 2, None,
+                                          None, None, None, None, None, heads, f, 1, act, 0.2, p,
+                                          0, None, None, None, 0, None)
+    assert rows_bwd(act=9) == EINVAL
+    assert rows_bwd(p=2.0) == EINVAL
+    assert rows_bwd(heads=65, f=1) == EUNS
+
+    ld = ctypes.c_int()
+    assert lib.gat_bwd_table_layout(8, 8, 1, ctypes.byref(ld)) == OK and ld.value == 64 + 32
+    assert lib.gat_bwd_table_layout(8, 8, 0, ctypes.byref(ld)) == OK and ld.value == 8 + 32
+    assert lib.gat_bwd_table_layout(0, 8, 0, ctypes.byref(ld)) == EINVAL
+    # recompute backward: a bad table stride is EINVAL, an unsupported shape EUNSUPPORTED
+    def tgt(f=8, ld_t=96, slope=0.2):
+        return lib.gat_bwd_targets(None, None, None, 0, 10, None, 64, None, None, None, None,
+                                   None, None, 8, f, 1, slope, 0.0, 0, None, None, None, ld_t, 0,
+                                   None)
+    assert tgt(ld_t=90) == EINVAL
+    assert tgt(f=7, ld_t=96) == EUNS  # f % 4 != 0 -> stored-coefficient path
+    assert tgt(slope=-0.5) == EUNS
+    parts = ctypes.c_int()
+    assert lib.gat_bwd_sources_parts(1000, 8, 8, ctypes.byref(parts)) == OK
+    assert parts.value % 4 == 0 and parts.value >= 4
+    # workspace queries
+    assert _lib.csc_workspace_size(10_000, 1000) > 4 * 4 * 10_000
+    assert _lib.weight_grad_workspace_size(44906, 50, 64) > 0
+    sz = ctypes.c_size_t()
+    assert lib.gat_sum_partials_workspace_size(100, 272, ctypes.byref(sz)) == OK and sz.value == 0
+    assert lib.gat_sum_partials_workspace_size(8192, 272, ctypes.byref(sz)) == OK
+    assert sz.value == 32 * 272 * 4
+    assert lib.gat_sum_partials(None, 8192, 272, None, None, 0, None) == _lib.GAT_EWORKSPACE
+    assert lib.gat_dropout_seed_next(None, None, None) == EINVAL
+
+
+C_DEMO = r"""
+#include <stdio.h>
+#include "gat_amd.h"
+int main(void) {
+    int ld = 0, s_off = 0, ld_t = 0;
+    size_t bytes = 0;
+    if (gat_abi_version() != GAT_ABI_VERSION) return 1;
+    if (gat_table_layout(8, 8, &ld, &s_off) != GAT_OK || ld != 72 || s_off != 64) return 2;
+    if (gat_bwd_table_layout(8, 8, 1, &ld_t) != GAT_OK || ld_t != 96) return 3;
+    if (gat_csr_workspace_size(1226368, 44906, &bytes) != GAT_OK || bytes == 0) return 4;
+    if (gat_project(0, -1, 4, 0, 0, 0, 0, 0, 0, 2, 2, 0, 4, 0, 2, 0, 0) != GAT_EINVAL) return 5;
+    printf("c-abi ok %d %d %zu\n", ld, ld_t, bytes);
+    return 0;
+}
+"""
+
+
+def test_header_compiles_and_links_from_plain_c(tmp_path):
+    """The boundary is consumable from C: a program compiled with gcc against
+    include/gat_amd.h alone links libgat_amd.so and calls the host-side entry
+    points (layouts, workspace sizes, argument validation)."""
+    from atmlgraphattentionnetworks_amd import _lib
+    src = tmp_path / "demo.c"
+    src.write_text(C_DEMO)
+    exe = tmp_path / "demo"
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    str(src), "-L", libdir, "-l:libgat_amd.so", "-Wl,-rpath," + libdir,
+                    "-o", str(exe)], check=True, capture_output=True, text=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert r.stdout.startswith("c-abi ok 72 96")
