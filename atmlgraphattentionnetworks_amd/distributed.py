@@ -287,6 +287,9 @@ def bench_distributed(args, metric: str):
     # gloo (barriers and the max-over-ranks reduction on the host): no RCCL
     # proxy threads compete with the launch thread while it is timed.  The RCCL
     # group is created afterwards, for the strong-scaling probe's all-gather.
+    # single node, rendezvous on 127.0.0.1: keep gloo on loopback rather than on
+    # whatever interface the (possibly unresolvable) hostname maps to
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     dist.init_process_group("gloo")
 
     w = WORKLOADS[args.workload]
