@@ -120,11 +120,38 @@ def train_step(layer, x, ei, n_edges: int, steps: int) -> dict:
         ev1.record(stream)
         ev1.synchronize()
     fwd_ms = ev0.elapsed_time(ev1) / steps
+    # the same step captured in a HIP graph (device-seeded dropout: a fresh mask
+    # per replay), as a trainer that graphs its step runs it
+    graph_ms = None
+    try:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                one()
+        torch.cuda.current_stream().wait_stream(s)
+        layer.zero_grad(set_to_none=True)
+        xg.grad = None
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            layer(xg, ei).backward(gout)
+        for _ in range(3):
+            g.replay()
+        ev0.record(stream)
+        for _ in range(steps):
+            g.replay()
+        ev1.record(stream)
+        ev1.synchronize()
+        graph_ms = ev0.elapsed_time(ev1) / steps
+    except Exception:  # noqa: BLE001  (the eager number above stands alone)
+        graph_ms = None
     layer.eval()
     return {"what": "layer forward (training mode, attention dropout 0.6) + HIP backward to x "
                     "and all parameters",
             "train_step_ms": step_ms, "forward_train_ms": fwd_ms,
-            "backward_ms": step_ms - fwd_ms, "train_edges_per_s": n_edges / (step_ms * 1e-3)}
+            "backward_ms": step_ms - fwd_ms, "train_edges_per_s": n_edges / (step_ms * 1e-3),
+            "train_step_graph_ms": graph_ms,
+            "train_edges_per_s_graph": None if not graph_ms else n_edges / (graph_ms * 1e-3)}
 
 
 def main():
