@@ -2407,6 +2407,17 @@ int gat_bwd_table_layout(int heads, int f, int concat, int* ld_t) {
     return GAT_OK;
 }
 
+// edges per chunk of the recompute backward kernels: the forward's thresholds;
+// GAT_BWD_U overrides (A/B knob)
+static int bwd_unroll(int hint) {
+    int u = hint <= 0 ? 8 : hint <= 32 ? 4 : hint <= 64 ? 8 : 16;
+    if (const char* v = std::getenv("GAT_BWD_U")) {
+        const int x = std::atoi(v);
+        u = (x == 4 || x == 16) ? x : 8;
+    }
+    return u;
+}
+
 static bool bwd_recompute_ok(int heads, int f, float slope, const float* wh, int ld_wh) {
     // GAT_BWD_KERNEL=stored|generic (A/B knob): force the stored-coefficient path
     if (const char* v = std::getenv("GAT_BWD_KERNEL"))
@@ -2436,7 +2447,7 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
     const DropArgs drop = make_drop(dropout_p, seed, seed_dev);
     const int hf = heads * f;
     const int g = next_pow2(hf / 4);
-    const int u = edges_per_row_hint > 0 && edges_per_row_hint <= 12 ? 4 : 8;
+    int u = bwd_unroll(edges_per_row_hint);
     const long long threads = (long long)rows * g;
     const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
 #define GAT_BT(G, UU)                                                                         \
@@ -2447,6 +2458,7 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
 #define GAT_BT_U(G)                      \
     case G:                              \
         if (u == 4) { GAT_BT(G, 4); }    \
+        else if (u == 16) { GAT_BT(G, 16); } \
         else { GAT_BT(G, 8); }           \
         break;
     switch (g) {
@@ -2487,8 +2499,7 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
     hipStream_t st = (hipStream_t)stream;
     const DropArgs drop = make_drop(dropout_p, seed, seed_dev);
     const int g = next_pow2(hf / 4);
-    int u = edges_per_row_hint > 0 && edges_per_row_hint <= 12 ? 4 : 8;
-    if (const char* v = std::getenv("GAT_BWD_U")) u = std::atoi(v) == 4 ? 4 : 8;  // A/B knob
+    int u = bwd_unroll(edges_per_row_hint);
     const dim3 grid(num_parts / 4), block(256);
 #define GAT_BS(G, UU)                                                                         \
     hipLaunchKernelGGL((k_bwd_sources<G, UU>), grid, block, 0, st, csc_ptr, csc_dst, csc_eid,  \
@@ -2497,6 +2508,7 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
 #define GAT_BS_U(G)                      \
     case G:                              \
         if (u == 4) { GAT_BS(G, 4); }    \
+        else if (u == 16) { GAT_BS(G, 16); } \
         else { GAT_BS(G, 8); }           \
         break;
     switch (g) {
