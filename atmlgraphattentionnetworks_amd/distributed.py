@@ -76,9 +76,9 @@ class HipOps:
     """The HIP kernels (default)."""
 
     @staticmethod
-    def alloc_table(n, heads, f, device, packed=True):
+    def alloc_table(n, heads, f, device, packed=True, wh_only=False):
         from .layer import alloc_table
-        return alloc_table(n, heads, f, device, packed=packed)
+        return alloc_table(n, heads, f, device, packed=packed, wh_only=wh_only)
 
     @staticmethod
     def project(x, pp, heads, f, table, s_dst):
@@ -90,6 +90,15 @@ class HipOps:
         from .layer import edge_aggregate
         return edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope, out=out,
                               pp=pp)
+
+
+def _default_score(layer) -> bool:
+    """LeakyReLU score activation with slope in [0, 1] (the fused-score kernels)."""
+    act = getattr(layer, "score_activation", None)
+    if act is None:
+        return True  # layers without the hook (test stand-ins) use the reference default
+    code, param = act()
+    return code == 0 and 0.0 <= param <= 1.0
 
 
 class ShardedGAT:
@@ -122,11 +131,21 @@ class ShardedGAT:
             n_table = csr.num_nodes
         lrp = (rp[self.r0:self.r1 + 1] - e0).to(torch.int32).contiguous()
         self.local = LocalCSR(lrp, col.contiguous(), self.n_local, e1 - e0, degree_order(lrp))
-        # allgather: one packed buffer [Wh | s_src] per node row, so a single
-        # collective moves both (zero-filled: padding rows are defined);
-        # replicate: the default separate layout (no collective to feed)
-        self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev,
-                                          packed=(exchange == "allgather"))
+        # allgather: the table rows every rank needs travel in ONE collective
+        # (zero-filled: padding rows are defined).  Where the edge kernel
+        # recomputes s_src from the gathered Wh row (LeakyReLU, f/4 a power of
+        # two) only Wh travels: 256-B, 128-B-aligned rows at H*F = 64 (the packed
+        # [Wh | s_src] row is 288 B and every gather straddles an extra line).
+        # Otherwise one packed buffer [Wh | s_src].  replicate: the default
+        # separate layout (no collective to feed).
+        hl = self.f // 4
+        self.wh_only = (exchange == "allgather" and self.f % 4 == 0 and hl > 0 and
+                        (hl & (hl - 1)) == 0 and _default_score(layer))
+        if self.wh_only:
+            self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev, wh_only=True)
+        else:
+            self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev,
+                                              packed=(exchange == "allgather"))
         self.s_dst_full = torch.empty(csr.num_nodes if exchange == "replicate" else self.n_local,
                                       self.heads, dtype=torch.float32, device=dev)
         width = self.heads * self.f if self.concat else self.f
@@ -296,6 +315,13 @@ def bench_distributed(args, metric: str):
     torch.manual_seed(0)
     layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
                                 concat=w.concat).to(dev).eval()
+
+    def layer_for(pw):
+        if pw is w:
+            return layer
+        torch.manual_seed(0)
+        return GraphAttentionLayer(pw.in_channels, pw.out_channels, num_heads=pw.heads,
+                                   concat=pw.concat).to(dev).eval()
     # this rank's block: seeds offset by rank (rank 0's block is the 1-GPU graph)
     x, ei = make_inputs(w, dev, x_seed=1 + 1000 * rank, edge_seed=2 + 1000 * rank)
     csr = get_csr(ei, x.size(0))
@@ -348,15 +374,23 @@ def bench_distributed(args, metric: str):
                 rccl = None
                 strong.append({"error": f"RCCL group: {type(exc).__name__}: {exc}"[:300]})
             if rccl is not None:
-                for ex in ("allgather", "replicate"):
+                probes = [(w, "allgather"), (w, "replicate")]
+                if (world > 1 or os.environ.get("GAT_BENCH_PROBE_REDDIT")) and w.name == "ppi":
+                    # the shape the all-gather is designed for: edge work
+                    # shrinks as 1/N while the exchanged table is 67 MB; its 1-GPU
+                    # reference is `bench.py --workload reddit`
+                    probes.append((WORKLOADS["reddit"], "allgather"))
+                for pw, ex in probes:
                     try:
-                        strong.append(_strong_probe(w, layer, dev, world, rank, ex,
-                                                    max(args.steps // 2, 5),
-                                                    max(args.warmup // 2, 2), not args.no_graph,
-                                                    group=rccl))
+                        r = _strong_probe(pw, layer_for(pw), dev, world, rank, ex,
+                                          max(args.steps // 2, 5), max(args.warmup // 2, 2),
+                                          not args.no_graph, group=rccl)
+                        r["workload"] = pw.name
+                        strong.append(r)
                     except Exception as exc:  # noqa: BLE001
-                        strong.append({"exchange": ex,
+                        strong.append({"workload": pw.name, "exchange": ex,
                                        "error": f"{type(exc).__name__}: {exc}"[:300]})
+                    torch.cuda.empty_cache()
 
     from bench import HBM_PEAK_GBS, edge_kernel_bytes, load_traffic  # noqa: E402
     alg = edge_kernel_bytes(n_block, csr.num_edges, w.heads, w.out_channels, w.concat)
@@ -379,7 +413,8 @@ def bench_distributed(args, metric: str):
                          "frac": ach / HBM_PEAK_GBS, "traffic": load_traffic(args.workload),
                          "kernel": "gat_edge_aggregate (rank 0 block)", "kernel_ms": edge_ms,
                          "algorithmic_bytes_per_launch": alg},
-            "strong_scaling": {"graph": f"one {w.name}-shape graph shared by {world} ranks",
+            "strong_scaling": {"graph": "one graph of the named workload's shape shared by "
+                                        f"{world} ranks, node-range partitioned",
                                "runs": strong},
         }
     dist.barrier()

@@ -87,20 +87,29 @@ class NodeTable(NamedTuple):
 
     Default layout: Wh [N, round_up(H*F, 4)] and a compact s_src [N, H].
     Packed layout (``packed=True``): one buffer [N, ld] holding both (one
-    collective moves both; see distributed.py), ``buf`` is that buffer."""
+    collective moves both; see distributed.py), ``buf`` is that buffer.
+    Wh-only layout (``wh_only=True``): ``s_src`` is None — for shapes whose
+    edge kernel recomputes s_src from the gathered Wh row (the library then
+    refuses, rather than guesses, if it would need s_src)."""
     wh: torch.Tensor
     ld_wh: int
-    s_src: torch.Tensor
+    s_src: Optional[torch.Tensor]
     ld_s: int
     buf: Optional[torch.Tensor] = None
 
     def rows(self, start: int, stop: int) -> "NodeTable":
         """The table restricted to rows [start, stop) (views, same strides)."""
-        return NodeTable(self.wh[start:stop], self.ld_wh, self.s_src[start:stop], self.ld_s,
+        return NodeTable(self.wh[start:stop], self.ld_wh,
+                         None if self.s_src is None else self.s_src[start:stop], self.ld_s,
                          None if self.buf is None else self.buf[start:stop])
 
 
-def alloc_table(n: int, heads: int, f: int, device, packed: bool = False) -> NodeTable:
+def alloc_table(n: int, heads: int, f: int, device, packed: bool = False,
+                wh_only: bool = False) -> NodeTable:
+    if wh_only:
+        hfp = (heads * f + 3) // 4 * 4
+        buf = torch.zeros(n, hfp, dtype=torch.float32, device=device)
+        return NodeTable(buf, hfp, None, heads, buf)
     if packed:
         ld, s_off = _lib.table_layout(heads, f)
         buf = torch.zeros(n, ld, dtype=torch.float32, device=device)
@@ -120,11 +129,14 @@ def project(x: torch.Tensor, pp: PackedParams, heads: int, f: int,
         table = alloc_table(n, heads, f, x.device)
     if s_dst is None:
         s_dst = torch.empty(n, heads, dtype=torch.float32, device=x.device)
+    s_src = table.s_src
+    if s_src is None:  # Wh-only table: the scores still have to go somewhere
+        s_src = torch.empty(n, heads, dtype=torch.float32, device=x.device)
     _lib.check(lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
                                pp.c_dst.data_ptr(), heads, f, table.wh.data_ptr(), table.ld_wh,
-                               table.s_src.data_ptr(), table.ld_s, s_dst.data_ptr(),
-                               _stream(x.device)), "gat_project")
+                               s_src.data_ptr(), heads if table.s_src is None else table.ld_s,
+                               s_dst.data_ptr(), _stream(x.device)), "gat_project")
     return table, s_dst
 
 
@@ -147,7 +159,8 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
     hint = csr.num_edges // max(csr.num_nodes, 1)
     _lib.check(lib.gat_edge_aggregate(
         csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
-        row_begin, rows, table.wh.data_ptr(), table.ld_wh, table.s_src.data_ptr(), table.ld_s,
+        row_begin, rows, table.wh.data_ptr(), table.ld_wh,
+        0 if table.s_src is None else table.s_src.data_ptr(), table.ld_s,
         0 if pp is None else pp.a_src.data_ptr(), 0 if pp is None else pp.c_src.data_ptr(),
         s_dst.data_ptr(), heads, f, int(concat), float(negative_slope), bias.data_ptr(),
         out.data_ptr(), 0 if lse is None else lse.data_ptr(), hint, _stream(table.wh.device)),
