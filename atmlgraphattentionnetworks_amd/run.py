@@ -100,7 +100,9 @@ class _GraphedStep:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                self.warmup_out.append(self._step())
+                # detached: a kept-alive autograd graph would carry its
+                # AccumulateGrad nodes (and their stream) into the capture
+                self.warmup_out.append(tuple(t.detach() for t in self._step()))
         torch.cuda.current_stream().wait_stream(s)
         self.graph = torch.cuda.CUDAGraph()
         optimizer.zero_grad(set_to_none=True)
