@@ -360,6 +360,167 @@ __device__ __forceinline__ float group_sum16(float v, int w) {
 }
 
 // ---------------------------------------------------------------------------
+// Projection, persistent and pipelined over row tiles (Fin <= 64, H*F <= 64);
+// an A/B alternative to k_project_wk (GAT_PROJ_KERNEL=persist), measured
+// slower at PPI shape.  The idea: k_project_wk launches one 64-row tile per
+// block and all of them fit on the chip at once, so every block loads, computes
+// and stores in lockstep.  Here a fixed grid of blocks loops over tiles
+// t = blockIdx, blockIdx + grid, ...: W and the epilogue parameters go to LDS
+// once per block, x tiles are double-buffered in LDS, and tile t + grid's x
+// is in flight (4 float4 per thread) while tile t is computed and stored.
+// LDS (floats): W [BN x fin] | x [2][64 x fin] | out [64 x (BN+4)] | params.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline int persist_lds_floats(int fin, int nt) {
+    const int bn = nt * 16;
+    const int w = (bn * fin + 3) & ~3, x = (64 * fin + 3) & ~3, o = 64 * (bn + 4);
+    return w + 2 * x + o + 3 * bn + 128;
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_project_persist(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh,
+    float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst) {
+    constexpr int BM = 64, BN = NT * 16, OS = BN + 4, XQ = BM * 64 / 1024;  // float4 / thread
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int wn = (BN * fin + 3) & ~3, xn = (BM * fin + 3) & ~3;
+    float* Ws = smem;
+    float* Xs0 = smem + wn;
+    float* Os = Xs0 + 2 * xn;
+    float* bs = Os + BM * OS;
+    float* a1s = bs + BN;
+    float* a2s = bs + 2 * BN;
+    float* c1s = bs + 3 * BN;
+    float* c2s = c1s + 64;
+    const int ntiles = (n + BM - 1) / BM;
+    const long long total = (long long)n * fin;
+    const long long last4 = (total & ~3LL) - 4;  // start of the array's last full float4
+
+    // x tile -> registers: unconditional float4 loads at addresses clamped into
+    // the array (rows past n are never stored); the <= 3 floats after the last
+    // full float4 come as scalars
+    f32x4 xv[XQ];
+    float xt[3];
+    auto load_x = [&](int t) {
+        const long long base = (long long)t * BM * fin;
+#pragma unroll
+        for (int q = 0; q < XQ; ++q) {
+            const long long i = base + 4LL * (tid + 256 * q);
+            xv[q] = *reinterpret_cast<const f32x4*>(X + (i < last4 ? i : last4));
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const long long i = (total & ~3LL) + j;
+            xt[j] = X[i < total ? i : total - 1];
+        }
+    };
+    auto store_x = [&](int t, float* Xs) {
+        const long long base = (long long)t * BM * fin;
+        const int cnt = (int)min((long long)BM * fin, total - base);
+        const int cnt4 = (int)(min(base + cnt, total & ~3LL) - base);  // full float4s
+#pragma unroll
+        for (int q = 0; q < XQ; ++q) {
+            const int i = 4 * (tid + 256 * q);
+            if (i < cnt4) *reinterpret_cast<f32x4*>(Xs + i) = xv[q];
+        }
+        if (tid == 0)
+            for (int j = 0; cnt4 + j < cnt && j < 3; ++j) Xs[cnt4 + j] = xt[j];
+    };
+
+    // once per block: W (rows >= HF zero) and the epilogue parameters
+    for (int i = tid; i < BN * fin; i += 256) Ws[i] = i < HF * fin ? W[i] : 0.f;
+    if (tid < BN) {
+        const bool ok = tid < HF;
+        const int cc = ok ? tid : 0;
+        const float bv = bW[cc], av1 = a1[cc], av2 = a2[cc];
+        bs[tid] = ok ? bv : 0.f;
+        a1s[tid] = ok ? av1 : 0.f;
+        a2s[tid] = ok ? av2 : 0.f;
+    }
+    if (tid < H) {
+        const float v1 = c1[tid], v2 = c2[tid];
+        c1s[tid] = v1;
+        c2s[tid] = v2;
+    }
+    int t = blockIdx.x;
+    if (t < ntiles) {
+        load_x(t);
+        store_x(t, Xs0);
+    }
+    __syncthreads();
+    const int hfp = round_up4(HF), c4n = hfp / 4;
+    for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
+        float* Xs = Xs0 + (it & 1) * xn;
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) load_x(tn);  // in flight during this tile's MFMAs and stores
+
+        f32x4 acc[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* xa = Xs + (w * 16 + cl) * fin + kq;
+        const float* wb = Ws + cl * fin + kq;
+        const int ks = fin / 4;
+        for (int s4 = 0; s4 < ks; ++s4) {
+            const float a = xa[4 * s4];
+#pragma unroll
+            for (int q = 0; q < NT; ++q)
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[q * 16 * fin + 4 * s4], acc[q],
+                                                              0, 0, 0);
+        }
+        if (fin & 3) {  // last partial k-step
+            const bool ok = 4 * ks + kq < fin;
+            const float a = ok ? xa[4 * ks] : 0.f;
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                const float b = ok ? wb[q * 16 * fin + 4 * ks] : 0.f;
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[q], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            const int cc = q * 16 + cl;
+            const float bb = bs[cc];  // Linear bias inside Wh (GAT.py:43); 0 past HF
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Os[(w * 16 + kq * 4 + i) * OS + cc] = acc[q][i] + bb;
+        }
+        __syncthreads();
+        const int row0 = t * BM, rows = min(BM, n - row0);
+        for (int idx = tid; idx < rows * c4n; idx += 256) {
+            const int r = idx / c4n, c4 = idx - r * c4n;
+            f32x4 v = *reinterpret_cast<const f32x4*>(Os + r * OS + 4 * c4);
+            if (4 * c4 + 3 >= HF) {  // zero the pad columns [HF, hfp)
+                if (4 * c4 + 0 >= HF) v.x = 0.f;
+                if (4 * c4 + 1 >= HF) v.y = 0.f;
+                if (4 * c4 + 2 >= HF) v.z = 0.f;
+                if (4 * c4 + 3 >= HF) v.w = 0.f;
+            }
+            *reinterpret_cast<f32x4*>(Wh + (size_t)(row0 + r) * ld_wh + 4 * c4) = v;
+        }
+        // attention Linears on the fp32 Wh (GAT.py:44-45): s = Wh_h . a_h + c_h
+        for (int idx = tid; idx < rows * H; idx += 256) {
+            const int r = idx / H, h = idx - r * H;
+            const float* o = Os + r * OS + h * F;
+            const float* p1 = a1s + h * F;
+            const float* p2 = a2s + h * F;
+            float v1 = 0.f, v2 = 0.f;
+            for (int f = 0; f < F; ++f) {
+                v1 = fmaf(o[f], p1[f], v1);
+                v2 = fmaf(o[f], p2[f], v2);
+            }
+            Ss[(size_t)(row0 + r) * ld_s + h] = v1 + c1s[h];
+            s_dst[(size_t)(row0 + r) * H + h] = v2 + c2s[h];
+        }
+        if (tn < ntiles) store_x(tn, Xs0 + ((it + 1) & 1) * xn);
+        __syncthreads();  // next tile's x in LDS; this tile's out reads done
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Projection, software-pipelined K loop (Fin > 64).  fp32 MFMA throughput
 // (157 TF) bounds a [N, Fin] x [Fin, 64] projection at large Fin (Reddit:
 // 18 GFLOP -> 115 us).  The K-tiled kernel reads its MFMA A operand straight
@@ -2056,6 +2217,36 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
                              reinterpret_cast<uintptr_t>(wh)) & 15) == 0;
     int wk_max = 64;  // GAT_PROJ_WK_MAX (A/B knob): largest fin for the whole-K kernel
     if (const char* v = std::getenv("GAT_PROJ_WK_MAX")) wk_max = std::atoi(v);
+    // persistent, tile-pipelined kernel: opt-in only (GAT_PROJ_KERNEL=persist).
+    // Measured slower than k_project_wk at PPI shape (16.2 vs 12.7 us hot, 21.7
+    // vs 16.7 us after the edge kernel): 2 blocks/CU keep too few loads in flight
+    const bool persist_ok = fin > 0 && fin <= 64 && nt <= 4 && n >= 64 && aligned16 &&
+                            pk != nullptr && std::strcmp(pk, "persist") == 0;
+    if (persist_ok) {
+        static int cus = 0;
+        if (cus == 0) {
+            int dev = 0, v = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+                cus = v;
+            if (cus <= 0) cus = 256;
+        }
+        const int ntiles = (n + 63) / 64;
+        const int blocks = ntiles < 2 * cus ? ntiles : 2 * cus;
+        const size_t lds = (size_t)persist_lds_floats(fin, nt) * sizeof(float);
+#define GAT_PERSIST_CASE(NT)                                                                  \
+    case NT:                                                                                  \
+        hipLaunchKernelGGL((k_project_persist<NT>), dim3(blocks), dim3(256), lds, st, x, n,    \
+                           fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh,    \
+                           s_src, ld_s, s_dst);                                               \
+        break;
+        switch (nt) {
+            GAT_PERSIST_CASE(1) GAT_PERSIST_CASE(2) GAT_PERSIST_CASE(3) GAT_PERSIST_CASE(4)
+            default: return GAT_EUNSUPPORTED;
+        }
+#undef GAT_PERSIST_CASE
+        return status_of(hipGetLastError());
+    }
     const bool wk_ok = fin > 0 && fin <= wk_max && aligned16 &&
                        (wk_lds > wk_out ? wk_lds : wk_out) <= 160 * 1024 &&
                        (pk == nullptr || std::strcmp(pk, "wk") == 0);

@@ -32,6 +32,8 @@ VARIANTS = {
     "gather_score": {"GAT_EDGE_SCORE": "gather"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
     "proj_direct": {"GAT_PROJ_KERNEL": "direct"},
+    "proj_persist": {"GAT_PROJ_KERNEL": "persist"},
+    "proj_pipe": {"GAT_PROJ_KERNEL": "pipe"},
     "v2": {"GAT_EDGE_V": "2"},
     "v4_natural": {"GAT_EDGE_V": "4", "GAT_EDGE_ORDER": "natural"},
 }
