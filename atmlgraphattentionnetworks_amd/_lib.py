@@ -17,7 +17,7 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 2
+GAT_ABI_VERSION = 3
 GAT_MAX_HEADS = 64
 GAT_MAX_HF = 256
 GAT_ACT_LEAKY_RELU = 0
@@ -39,6 +39,12 @@ SIGNATURES = {
     "gat_edge_aggregate": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int, _c_vp,
                                     _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
                                     _c_float, _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
+    "gat_project_sliced": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                    _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_int, _c_vp,
+                                    _c_vp]),
+    "gat_edge_aggregate_sliced": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
+                                           _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_float,
+                                           _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_csr_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csr_build": (_c_int, [_c_vp, _c_ll, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, ctypes.c_size_t,
                                _c_vp, _c_vp]),

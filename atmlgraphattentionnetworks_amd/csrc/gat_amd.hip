@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) void k_project_pipe(
     const float* __restrict__ a1, const float* __restrict__ c1,
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
-    float* __restrict__ s_dst) {
+    float* __restrict__ s_dst, int slice_w, long long slice_stride) {
     constexpr int BK = 64, KS = BK / 4, BN = NT * 16, BM = 128;
     constexpr int WL = BN * BK / 256;  // W-tile elements per thread
     constexpr int XL = BM * BK / 256;  // x-tile elements per thread (32)
@@ -620,12 +620,14 @@ __global__ __launch_bounds__(256) void k_project_pipe(
         for (int t = 0; t < NT; ++t) {
             const int cc = t * 16 + cl;
             const float bb = cc < HF ? bW[cc] : 0.f;
+            const int sg = cc / slice_w;  // slice plane of this column (0 unsliced)
+            float* whc = Wh + (size_t)sg * (size_t)slice_stride + (cc - sg * slice_w);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float v = acc[g][t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
                 acc[g][t][i] = v;
                 const int rr = rbase + i;
-                if (rr < n && cc < hfp) Wh[(size_t)rr * ld_wh + cc] = v;
+                if (rr < n && cc < hfp) whc[(size_t)rr * ld_wh] = v;
             }
         }
         // scores: head = F consecutive lanes of one 16-column tile (F | 16)
@@ -805,7 +807,8 @@ __global__ __launch_bounds__(256) void k_project_wk(
     const float* __restrict__ a1, const float* __restrict__ c1,
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ Wh, int ld_wh,
-    float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst) {
+    float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst,
+    int slice_w, long long slice_stride) {
     constexpr int BM = 64, BN = NT * 16;
     constexpr int OS = BN + 4;  // output-tile stride: float4-aligned rows, no write conflicts
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -916,9 +919,14 @@ __global__ __launch_bounds__(256) void k_project_wk(
         for (int i = 0; i < 4; ++i) Os[(w * 16 + kq * 4 + i) * OS + cc] = acc[t][i] + bb;
     }
     __syncthreads();
+    // Wh stores: slice-major so consecutive lanes fill one slice plane's rows
+    // (unsliced: slice_w >= hfp, one slice, the plain row-major order)
     const int hfp = round_up4(HF), c4n = hfp / 4;
+    const int cs4 = (slice_w < hfp ? slice_w : hfp) / 4;  // float4s per slice row
     for (int idx = tid; idx < rows * c4n; idx += 256) {
-        const int r = idx / c4n, c4 = idx - r * c4n;
+        const int g = idx / (rows * cs4), rem = idx - g * rows * cs4;
+        const int r = rem / cs4, q = rem - r * cs4;
+        const int c4 = g * cs4 + q;
         f32x4 v = *reinterpret_cast<const f32x4*>(Os + r * OS + 4 * c4);
         if (4 * c4 + 3 >= HF) {  // zero the pad columns [HF, hfp)
             if (4 * c4 + 0 >= HF) v.x = 0.f;
@@ -926,7 +934,8 @@ __global__ __launch_bounds__(256) void k_project_wk(
             if (4 * c4 + 2 >= HF) v.z = 0.f;
             if (4 * c4 + 3 >= HF) v.w = 0.f;
         }
-        *reinterpret_cast<f32x4*>(Wh + (size_t)(row0 + r) * ld_wh + 4 * c4) = v;
+        *reinterpret_cast<f32x4*>(Wh + (size_t)g * (size_t)slice_stride +
+                                  (size_t)(row0 + r) * ld_wh + 4 * q) = v;
     }
     // attention Linears on the fp32 Wh (GAT.py:44-45): s = Wh_h . a_h + c_h
     for (int idx = tid; idx < rows * H; idx += 256) {
@@ -1135,17 +1144,26 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const float* __restrict__ a_src, const float* __restrict__ c_src,
     const float* __restrict__ s_dst, int H, int F, int HF, int concat, float slope,
     const float* __restrict__ bias, float* __restrict__ out, int ld_out,
-    float* __restrict__ lse, DropArgs drop_arg, float* __restrict__ y_heads) {
+    float* __restrict__ lse, DropArgs drop_arg, float* __restrict__ y_heads,
+    int nslices, int slice_w, long long slice_stride) {
     const DropArgs drop = resolve_drop(drop_arg);
     constexpr int CL = (U + G - 1) / G;  // col values held per lane per chunk
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
-    const int pos = row_begin + (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    // sliced node table (nslices > 1): block b works on column slice b % nslices,
+    // so with round-robin block placement one XCD gathers from one slice plane
+    // only — an [N, slice_w] plane small enough to stay in that XCD's L2
+    const int sl = nslices > 1 ? (int)(blockIdx.x % (unsigned)nslices) : 0;
+    const unsigned blk = nslices > 1 ? blockIdx.x / (unsigned)nslices : blockIdx.x;
+    const int pos = row_begin + (int)((blk * (size_t)blockDim.x + threadIdx.x) / G);
     if (pos >= row_end) return;
     const int r = order != nullptr ? order[pos] : pos;
-    const bool c_ok = 4 * V * c < HF;
-    const int coff = c_ok ? 4 * V * c : 0;
+    const int sw = nslices > 1 ? slice_w : HF;  // columns this block's groups own
+    const bool c_ok = 4 * V * c < sw;
+    const int loff = c_ok ? 4 * V * c : 0;      // column within the slice
+    const int coff = sl * slice_w + loff;       // column of the layer output
+    const float* __restrict__ Whs = Wh + (size_t)sl * (size_t)slice_stride + loff;
     const int h = coff / F;
     f32x4 a4[V];
     float c1 = 0.f;
@@ -1188,7 +1206,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         float s[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const float* row = Wh + (size_t)j[u] * ld_wh + coff;
+            const float* row = Whs + (size_t)j[u] * ld_wh;
 #pragma unroll
             for (int q = 0; q < V; ++q) v[u][q] = *reinterpret_cast<const f32x4*>(row + 4 * q);
             if constexpr (!FUSED) s[u] = Ss[(size_t)j[u] * ld_s + h];
@@ -2194,22 +2212,33 @@ int gat_table_layout(int heads, int f, int* ld, int* s_off) {
     return GAT_OK;
 }
 
-int gat_project(const float* x, int n, int fin, const float* w, const float* b,
-                const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,
-                int heads, int f, float* wh, int ld_wh, float* s_src, int ld_s, float* s_dst,
-                void* stream) {
-    if (n < 0 || fin < 0 || heads <= 0 || f <= 0) return GAT_EINVAL;
+// slices == 1: Wh row-major [n, ld_wh].  slices > 1: `slices` planes of
+// [n, ld_wh = hf / slices] at wh + g * n * ld_wh (only the whole-K and the
+// pipelined kernels write that layout).
+static int project_impl(const float* x, int n, int fin, const float* w, const float* b,
+                        const float* a_src, const float* c_src, const float* a_dst,
+                        const float* c_dst, int heads, int f, int slices, float* wh, int ld_wh,
+                        float* s_src, int ld_s, float* s_dst, void* stream) {
+    if (n < 0 || fin < 0 || heads <= 0 || f <= 0 || slices <= 0) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
-    if (ld_wh < round_up4(hf) || (ld_wh & 3) || ld_s < heads) return GAT_EINVAL;
+    const bool sliced = slices > 1;
+    if (sliced) {
+        if (hf % slices != 0 || ((hf / slices) & 3) || ld_wh != hf / slices || ld_s < heads)
+            return GAT_EINVAL;
+    } else if (ld_wh < round_up4(hf) || (ld_wh & 3) || ld_s < heads) {
+        return GAT_EINVAL;
+    }
     if (n == 0) return GAT_OK;
+    const int slice_w = sliced ? ld_wh : round_up4(hf);
+    const long long slice_stride = sliced ? (long long)n * ld_wh : 0;
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
     const int nt = (hf + 15) / 16;
     // GAT_PROJ_KERNEL (A/B knob): "wk" (default for fin <= 128: whole K in LDS),
     // "tiled" (K-tiled, shuffle epilogue; default for larger fin), "lds"
     // (K-tiled, LDS epilogue), "direct" (register-direct, F a power of two)
-    const char* pk = std::getenv("GAT_PROJ_KERNEL");
+    const char* pk = sliced ? nullptr : std::getenv("GAT_PROJ_KERNEL");
     const bool pow2_f = next_pow2(f) == f;
     const size_t wk_lds = (size_t)wk_lds_floats(fin, nt) * sizeof(float);
     const size_t wk_out = 0;  // the output tile is inside wk_lds_floats
@@ -2255,7 +2284,8 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
 #define GAT_WK_CASE(NT)                                                                       \
     case NT:                                                                                  \
         hipLaunchKernelGGL((k_project_wk<NT>), grid, block, lds, st, x, n, fin, w, b, a_src,  \
-                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst); \
+                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
+                           slice_w, slice_stride);                                            \
         break;
         switch (nt) {
             GAT_WK_CASE(1) GAT_WK_CASE(2) GAT_WK_CASE(3) GAT_WK_CASE(4)
@@ -2277,7 +2307,8 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
 #define GAT_PIPE_CASE(NT)                                                                     \
     case NT:                                                                                  \
         hipLaunchKernelGGL((k_project_pipe<NT>), gp, bp, 0, st, x, n, fin, w, b, a_src, c_src, \
-                           a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst);        \
+                           a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,         \
+                           slice_w, slice_stride);                                            \
         break;
         switch (nt) {
             GAT_PIPE_CASE(1) GAT_PIPE_CASE(2) GAT_PIPE_CASE(3) GAT_PIPE_CASE(4)
@@ -2286,6 +2317,7 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
 #undef GAT_PIPE_CASE
         return status_of(hipGetLastError());
     }
+    if (sliced) return GAT_EUNSUPPORTED;  // the kernels below write row-major Wh only
     if (pow2_f && pk != nullptr && std::strcmp(pk, "direct") == 0) {
         int tw = nt < 2 ? nt : 2;
         if (f / 16 > tw) tw = f / 16;
@@ -2330,18 +2362,49 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
     return status_of(hipGetLastError());
 }
 
+int gat_project(const float* x, int n, int fin, const float* w, const float* b,
+                const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,
+                int heads, int f, float* wh, int ld_wh, float* s_src, int ld_s, float* s_dst,
+                void* stream) {
+    return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, 1, wh, ld_wh,
+                        s_src, ld_s, s_dst, stream);
+}
+
+int gat_project_sliced(const float* x, int n, int fin, const float* w, const float* b,
+                       const float* a_src, const float* c_src, const float* a_dst,
+                       const float* c_dst, int heads, int f, int slices, float* wh,
+                       float* s_src, int ld_s, float* s_dst, void* stream) {
+    if (slices <= 0 || heads <= 0 || f <= 0 || (heads * f) % slices != 0) return GAT_EINVAL;
+    return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
+                        heads * f / slices, s_src, ld_s, s_dst, stream);
+}
+
 static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row_order,
                                int row_begin, int row_end, const float* wh, int ld_wh,
                                const float* s_src, int ld_s, const float* a_src,
                                const float* c_src, const float* s_dst, int heads, int f,
                                int concat, int act, float negative_slope, const float* bias,
                                float* out, float* lse, float* y_heads, DropArgs drop,
-                               int edges_per_row_hint, void* stream) {
+                               int edges_per_row_hint, void* stream, int nslices = 1,
+                               long long slice_stride = 0) {
     if (act < GAT_ACT_LEAKY_RELU || act > GAT_ACT_HEAD_SOFTMAX) return GAT_EINVAL;
-    if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin) return GAT_EINVAL;
+    if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin || nslices <= 0)
+        return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
-    if (ld_wh < round_up4(hf) || (ld_wh & 3)) return GAT_EINVAL;
+    const bool sliced = nslices > 1;
+    if (sliced) {
+        // slice planes of ld_wh = hf / nslices columns, whole heads or whole
+        // float4 groups of one head; concat + fused LeakyReLU score only
+        if (hf % nslices != 0 || ld_wh != hf / nslices || (ld_wh & 3) || slice_stride <= 0)
+            return GAT_EINVAL;
+        if (!concat || s_src != nullptr || act != GAT_ACT_LEAKY_RELU || lse != nullptr ||
+            y_heads != nullptr)
+            return GAT_EUNSUPPORTED;
+    } else if (ld_wh < round_up4(hf) || (ld_wh & 3)) {
+        return GAT_EINVAL;
+    }
+    const int slice_w = sliced ? ld_wh : round_up4(hf);
     if (s_src != nullptr && ld_s < heads) return GAT_EINVAL;
     const bool have_a = a_src != nullptr && c_src != nullptr;
     if (s_src == nullptr && !have_a) return GAT_EINVAL;
@@ -2364,12 +2427,15 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
     while (vv > 1 && f % (4 * vv) != 0) vv >>= 1;
     const int hl = f / (4 * vv);  // lanes per head
     const bool pow2_hl = (f % (4 * vv) == 0) && next_pow2(hl) == hl;
-    const int g = next_pow2((hf + 4 * vv - 1) / (4 * vv));
+    const int gcols = sliced ? slice_w : hf;  // columns one lane group owns
+    const int g = next_pow2((gcols + 4 * vv - 1) / (4 * vv));
     const bool grp_ok = (f % 4 == 0) && (concat || pow2_hl) && slope_ok;
     // fused source score: the head's lanes must form an aligned power-of-two block
     bool fused = grp_ok && pow2_hl && have_a;
     if (fused && s_src != nullptr) fused = kernel_choice("GAT_EDGE_SCORE", "fused", "gather");
     if (s_src == nullptr && !fused) return GAT_EUNSUPPORTED;
+    // a slice holds whole heads (the fused score sums a head inside one group)
+    if (sliced && (!fused || slice_w % f != 0)) return GAT_EUNSUPPORTED;
     if (grp_ok && (s_src == nullptr || kernel_choice("GAT_EDGE_KERNEL", "group", "generic"))) {
         // edges per chunk: short rows want short chunks (less padding), long rows
         // more loads in flight; GAT_EDGE_U overrides
@@ -2378,11 +2444,13 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
               : edges_per_row_hint <= 64 ? 8 : 16;
         if (const char* eu = std::getenv("GAT_EDGE_U")) u = std::atoi(eu);
         const long long threads = (long long)rows * g;
-        const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+        const long long blocks = ((threads + 255) / 256) * nslices;
+        if (blocks >= (1LL << 31)) return GAT_EUNSUPPORTED;
+        const dim3 grid((unsigned)blocks), block(256);
 #define GAT_GRP_ARGS                                                                          \
     grid, block, 0, st, rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s,    \
         a_src, c_src, s_dst, heads, f, hf, concat, negative_slope, bias, out, ld_out, lse,     \
-        drop, y_heads
+        drop, y_heads, nslices, slice_w, slice_stride
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
     if (fused)                                                                        \
         hipLaunchKernelGGL((k_edge_grp<G, UU, VV, true>), GAT_GRP_ARGS);              \
@@ -2455,6 +2523,22 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
                                ld_s, a_src, c_src, s_dst, heads, f, concat, GAT_ACT_LEAKY_RELU,
                                negative_slope, bias, out, lse, nullptr, make_drop(0.f, 0ull),
                                edges_per_row_hint, stream);
+}
+
+int gat_edge_aggregate_sliced(const int* rowptr, const int* col, const int* row_order,
+                              int row_begin, int row_end, const float* wh, int n_table,
+                              int slices, const float* a_src, const float* c_src,
+                              const float* s_dst, int heads, int f, float negative_slope,
+                              const float* bias, float* out, int edges_per_row_hint,
+                              void* stream) {
+    if (slices <= 1 || heads <= 0 || f <= 0 || n_table <= 0 || (heads * f) % slices != 0)
+        return GAT_EINVAL;
+    if (a_src == nullptr || c_src == nullptr) return GAT_EINVAL;
+    const int sw = heads * f / slices;
+    return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, sw, nullptr, 0,
+                               a_src, c_src, s_dst, heads, f, 1, GAT_ACT_LEAKY_RELU,
+                               negative_slope, bias, out, nullptr, nullptr, make_drop(0.f, 0ull),
+                               edges_per_row_hint, stream, slices, (long long)n_table * sw);
 }
 
 int gat_edge_aggregate_ex(const int* rowptr, const int* col, const int* row_order, int row_begin,

@@ -29,7 +29,7 @@ from . import _lib
 from .graph import CSRGraph, get_csr
 
 __all__ = ["GraphAttentionLayer", "GraphAttentionLayerActivationTest", "score_activation_code",
-           "PackedParams", "pack_params", "gat_forward", "NodeTable",
+           "PackedParams", "pack_params", "gat_forward", "wh_slices", "NodeTable",
            "alloc_table", "project", "edge_aggregate"]
 
 
@@ -90,22 +90,34 @@ class NodeTable(NamedTuple):
     collective moves both; see distributed.py), ``buf`` is that buffer.
     Wh-only layout (``wh_only=True``): ``s_src`` is None — for shapes whose
     edge kernel recomputes s_src from the gathered Wh row (the library then
-    refuses, rather than guesses, if it would need s_src)."""
+    refuses, rather than guesses, if it would need s_src).
+    Sliced layout (``slices > 1``): Wh as ``slices`` column planes
+    [slices, N, ld_wh = H*F/slices] (gat_project_sliced / gat_edge_aggregate_sliced)."""
     wh: torch.Tensor
     ld_wh: int
     s_src: Optional[torch.Tensor]
     ld_s: int
     buf: Optional[torch.Tensor] = None
+    slices: int = 1
 
     def rows(self, start: int, stop: int) -> "NodeTable":
         """The table restricted to rows [start, stop) (views, same strides)."""
+        if self.slices > 1:
+            raise ValueError("row views of a sliced node table are not supported")
         return NodeTable(self.wh[start:stop], self.ld_wh,
                          None if self.s_src is None else self.s_src[start:stop], self.ld_s,
                          None if self.buf is None else self.buf[start:stop])
 
 
 def alloc_table(n: int, heads: int, f: int, device, packed: bool = False,
-                wh_only: bool = False) -> NodeTable:
+                wh_only: bool = False, slices: int = 1) -> NodeTable:
+    if slices > 1:
+        if packed or wh_only or (heads * f) % slices:
+            raise ValueError("a sliced table is Wh planes plus a compact s_src")
+        sw = heads * f // slices
+        wh = torch.empty(slices, n, sw, dtype=torch.float32, device=device)
+        s_src = torch.empty(n, heads, dtype=torch.float32, device=device)
+        return NodeTable(wh, sw, s_src, heads, None, slices)
     if wh_only:
         hfp = (heads * f + 3) // 4 * 4
         buf = torch.zeros(n, hfp, dtype=torch.float32, device=device)
@@ -132,6 +144,13 @@ def project(x: torch.Tensor, pp: PackedParams, heads: int, f: int,
     s_src = table.s_src
     if s_src is None:  # Wh-only table: the scores still have to go somewhere
         s_src = torch.empty(n, heads, dtype=torch.float32, device=x.device)
+    if table.slices > 1:
+        _lib.check(lib.gat_project_sliced(
+            x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(),
+            pp.c_src.data_ptr(), pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
+            table.slices, table.wh.data_ptr(), s_src.data_ptr(), table.ld_s, s_dst.data_ptr(),
+            _stream(x.device)), "gat_project_sliced")
+        return table, s_dst
     _lib.check(lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
                                pp.c_dst.data_ptr(), heads, f, table.wh.data_ptr(), table.ld_wh,
@@ -157,6 +176,16 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
     if order is not None and os.environ.get("GAT_EDGE_ORDER") == "natural":  # A/B knob
         order = None
     hint = csr.num_edges // max(csr.num_nodes, 1)
+    if table.slices > 1:
+        if pp is None or lse is not None:
+            raise ValueError("the sliced edge kernel recomputes s_src (pp) and has no lse")
+        _lib.check(lib.gat_edge_aggregate_sliced(
+            csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
+            row_begin, rows, table.wh.data_ptr(), table.wh.size(1), table.slices,
+            pp.a_src.data_ptr(), pp.c_src.data_ptr(), s_dst.data_ptr(), heads, f,
+            float(negative_slope), bias.data_ptr(), out.data_ptr(), hint,
+            _stream(table.wh.device)), "gat_edge_aggregate_sliced")
+        return out
     _lib.check(lib.gat_edge_aggregate(
         csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
         row_begin, rows, table.wh.data_ptr(), table.ld_wh,
@@ -168,13 +197,50 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
     return out
 
 
+def wh_slices(heads: int, f: int, concat: bool, negative_slope: float,
+              edges_per_row: int = 0) -> int:
+    """Number of column planes for the eval forward's node table
+    (``gat_project_sliced`` / ``gat_edge_aggregate_sliced``), 1 = row-major.
+
+    A plane holds whole heads; the edge kernel needs concat, LeakyReLU with
+    slope in [0, 1] and f/4 a power of two.  Default: 128-byte plane rows (one
+    cache line per gathered row, HF = 64 -> 2 planes) once rows average >= 16
+    in-edges.  Measured with ``tools/slice_probe.py`` (interleaved, graph
+    replay): edge kernel PPI 33.9 -> 30.0 us, Reddit scale 3.21 -> 2.49 ms;
+    planes of 64 or 32 B rows are slower than row-major (more cache lines per
+    wave instruction), and at ogbn-arxiv's 8 edges per row 2 planes lose
+    (56.6 -> 61.8 us: each plane re-reads the row's indices and bookkeeping).
+    ``GAT_WH_SLICES`` (A/B knob) overrides the default."""
+    hf = heads * f
+    env = os.environ.get("GAT_WH_SLICES")
+    if env is not None:
+        s = int(env)
+    elif hf % _PLANE_COLS == 0 and edges_per_row >= _MIN_SLICED_EPR:
+        s = hf // _PLANE_COLS
+    else:
+        s = 1
+    if s <= 1 or not concat or not (0.0 <= negative_slope <= 1.0):
+        return 1
+    if f % 4 or (f // 4) & (f // 4 - 1):
+        return 1
+    while s > 1 and (heads % s or (hf // s) % 4):
+        s -= 1
+    return max(s, 1)
+
+
+_PLANE_COLS = 32        # 128-byte plane rows
+_MIN_SLICED_EPR = 16    # average in-edges per row below which row-major wins
+
+
 def gat_forward(x: torch.Tensor, csr: CSRGraph, pp: PackedParams, bias: torch.Tensor,
                 heads: int, f: int, concat: bool, negative_slope: float = 0.2) -> torch.Tensor:
     """Layer forward on prepared inputs: projection + edge kernel (2 launches).
 
     Lean host path (it is on the critical path for graphs the size of PPI,
     where the GPU work is ~50 us): one workspace allocation holding
-    Wh | s_src | s_dst, one output allocation, two C-ABI calls."""
+    Wh | s_src | s_dst, one output allocation, two C-ABI calls.  With
+    ``wh_slices(...) > 1`` Wh is stored as column planes (``gat_amd.h``,
+    sliced node table) and the edge kernel runs one plane per workgroup."""
     lib = _lib.load()
     n, fin = x.shape
     hf = heads * f
@@ -186,17 +252,34 @@ def gat_forward(x: torch.Tensor, csr: CSRGraph, pp: PackedParams, bias: torch.Te
     p_ss = p_wh + 4 * n * hfp
     p_sd = p_ss + 4 * n * heads
     stream = torch._C._cuda_getCurrentRawStream(dev.index)
+    order = csr.order
+    p_order = 0 if order is None else order.data_ptr()
+    hint = csr.num_edges // max(n, 1)
+    slices = wh_slices(heads, f, concat, negative_slope, hint)
+    if slices > 1:
+        rc = lib.gat_project_sliced(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                                    pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+                                    pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f, slices,
+                                    p_wh, p_ss, heads, p_sd, stream)
+        if rc == 0:
+            rc = lib.gat_edge_aggregate_sliced(
+                csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, p_wh, n, slices,
+                pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, heads, f,
+                float(negative_slope), bias.data_ptr(), out.data_ptr(), hint, stream)
+            if rc:
+                _lib.check(rc, "gat_edge_aggregate_sliced")
+            return out
+        if rc != _lib.GAT_EUNSUPPORTED:  # nothing was launched: row-major below
+            _lib.check(rc, "gat_project_sliced")
     rc = lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                          pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
                          pp.c_dst.data_ptr(), heads, f, p_wh, hfp, p_ss, heads, p_sd, stream)
     if rc:
         _lib.check(rc, "gat_project")
-    order = csr.order
     rc = lib.gat_edge_aggregate(
-        csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(), 0,
+        csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0,
         n, p_wh, hfp, p_ss, heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, heads, f,
-        int(concat), float(negative_slope), bias.data_ptr(), out.data_ptr(), 0,
-        csr.num_edges // max(n, 1), stream)
+        int(concat), float(negative_slope), bias.data_ptr(), out.data_ptr(), 0, hint, stream)
     if rc:
         _lib.check(rc, "gat_edge_aggregate")
     return out

@@ -185,7 +185,7 @@ def main():
         return bench_distributed(args, METRIC)
 
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
-    from atmlgraphattentionnetworks_amd.layer import alloc_table, edge_aggregate, project
+    from atmlgraphattentionnetworks_amd.layer import alloc_table, edge_aggregate, project, wh_slices
     from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
 
     dev = torch.device("cuda", 0)
@@ -236,7 +236,11 @@ def main():
 
         # edge kernel alone, HIP events on the stream it is launched on
         pp = layer.packed()
-        table, s_dst = project(x, pp, w.heads, w.out_channels)
+        # the table layout the layer's forward uses (layer.wh_slices)
+        slices = wh_slices(w.heads, w.out_channels, w.concat, layer.negative_slope,
+                           n_edges // max(n, 1))
+        table, s_dst = project(x, pp, w.heads, w.out_channels,
+                               table=alloc_table(n, w.heads, w.out_channels, dev, slices=slices))
         out = torch.empty(n, w.heads * w.out_channels if w.concat else w.out_channels,
                           device=dev)
         for _ in range(5):
@@ -288,7 +292,9 @@ def main():
                    "parallelism": "single GPU", "launch": "hipGraph" if graph else "eager"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "gat_edge_aggregate (k_edge_grp)", "kernel_ms": edge_ms,
+                     "kernel": ("gat_edge_aggregate_sliced (k_edge_grp, %d column planes)" % slices
+                                if slices > 1 else "gat_edge_aggregate (k_edge_grp)"),
+                     "kernel_ms": edge_ms,
                      "algorithmic_bytes_per_launch": alg_bytes},
         "breakdown_ms": {"project": proj_ms, "edge": edge_ms, "csr_build_once": csr_ms},
         "projection": {"bound": "mfma", "achieved": proj_tflops, "peak": MFMA_F32_PEAK_TFLOPS,

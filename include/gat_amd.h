@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 2
+#define GAT_ABI_VERSION 3
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -114,6 +114,37 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
                        const float* a_src, const float* c_src, const float* s_dst, int heads,
                        int f, int concat, float negative_slope, const float* bias, float* out,
                        float* lse, int edges_per_row_hint, void* stream);
+
+/*
+ * Sliced node table: the same projection (GAT.py:42-52) and edge aggregation
+ * (GAT.py:53-67, +bias GAT.py:54) as gat_project / gat_edge_aggregate, with Wh
+ * stored as `slices` column planes instead of row-major rows.  Plane g holds
+ * columns [g*sw, (g+1)*sw) of every node, sw = heads*f/slices, as a row-major
+ * [n_table, sw] array at wh + g*n_table*sw.  The edge kernel runs one plane per
+ * workgroup (consecutive workgroups take consecutive planes), so with the
+ * hardware's round-robin workgroup placement each XCD gathers from one plane,
+ * which is 1/slices of the table and can stay resident in that XCD's L2.
+ * Results equal the row-major entry points' (same arithmetic, same order).
+ *
+ * gat_project_sliced: as gat_project with ld_wh = sw (heads*f % slices == 0,
+ *   sw % 4 == 0); n_table = n.  GAT_EUNSUPPORTED for shapes whose projection
+ *   kernel writes row-major only (fin > 64 needs f a power of two <= 16 and
+ *   heads*f <= 64).
+ * gat_edge_aggregate_sliced: concat only, LeakyReLU slope in [0, 1], sw % f == 0
+ *   (whole heads per plane), f % 4 == 0 and f/4 a power of two; the source
+ *   score is recomputed from the gathered plane row (a_src, c_src required).
+ *   n_table = rows of each plane (the n passed to gat_project_sliced).
+ */
+int gat_project_sliced(const float* x, int n, int fin, const float* w, const float* b,
+                       const float* a_src, const float* c_src, const float* a_dst,
+                       const float* c_dst, int heads, int f, int slices, float* wh,
+                       float* s_src, int ld_s, float* s_dst, void* stream);
+int gat_edge_aggregate_sliced(const int* rowptr, const int* col, const int* row_order,
+                              int row_begin, int row_end, const float* wh, int n_table,
+                              int slices, const float* a_src, const float* c_src,
+                              const float* s_dst, int heads, int f, float negative_slope,
+                              const float* bias, float* out, int edges_per_row_hint,
+                              void* stream);
 
 /* Workspace bytes gat_csr_build needs for (num_edges, num_nodes). */
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);

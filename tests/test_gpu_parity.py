@@ -36,13 +36,19 @@ VARIANTS = {
     "proj_pipe": {"GAT_PROJ_KERNEL": "pipe"},
     "v2": {"GAT_EDGE_V": "2"},
     "v4_natural": {"GAT_EDGE_V": "4", "GAT_EDGE_ORDER": "natural"},
+    # sliced node table (gat_*_sliced); shapes it does not take run row-major
+    "sliced2": {"GAT_WH_SLICES": "2"},
+    "sliced4_u16": {"GAT_WH_SLICES": "4", "GAT_EDGE_U": "16"},
+    "sliced8": {"GAT_WH_SLICES": "8"},
+    "sliced8_v2": {"GAT_WH_SLICES": "8", "GAT_EDGE_V": "2"},
+    "sliced4_proj_pipe": {"GAT_WH_SLICES": "4", "GAT_PROJ_WK_MAX": "0"},
 }
 
 
 @pytest.fixture(params=list(VARIANTS))
 def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
-              "GAT_EDGE_ORDER"):
+              "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -204,3 +210,70 @@ def test_ppi_shape_full_size_vs_oracle():
                     x, ei)
     ref = gat_layer_forward_from_state(state, x.cpu(), ei.cpu(), w.heads, w.concat)
     torch.testing.assert_close(out, ref, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.parametrize("slices,H,F,fin", [(8, 8, 8, 50), (4, 8, 8, 50), (2, 4, 8, 3),
+                                            (4, 4, 8, 128), (8, 8, 8, 602), (3, 3, 8, 20),
+                                            (4, 4, 16, 50)])
+def test_sliced_table_equals_row_major(slices, H, F, fin, monkeypatch):
+    """gat_project_sliced + gat_edge_aggregate_sliced take this shape (status 0,
+    checked directly) and give the row-major path's output bit for bit: the
+    same per-lane arithmetic on a different table layout."""
+    from atmlgraphattentionnetworks_amd import _lib
+    from atmlgraphattentionnetworks_amd.layer import wh_slices
+    n, e = 1500, 30000
+    x, ei, state = random_case(n, e, fin, H, F, True, seed=slices * 100 + H)
+    layer = layer_from_state(state, fin, F, H, True)
+    monkeypatch.setenv("GAT_WH_SLICES", str(slices))
+    assert wh_slices(H, F, True, 0.2) == slices
+    pp = layer.packed()
+    xd = x.to(dev())
+    wh = torch.empty(n * H * F, device=dev())
+    ss = torch.empty(n * H, device=dev())
+    sd = torch.empty(n * H, device=dev())
+    lib = _lib.load()
+    rc = lib.gat_project_sliced(xd.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                                pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
+                                pp.c_dst.data_ptr(), H, F, slices, wh.data_ptr(), ss.data_ptr(),
+                                H, sd.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    a = run_layer(layer, x, ei)
+    monkeypatch.setenv("GAT_WH_SLICES", "1")
+    b = run_layer(layer, x, ei)
+    assert torch.equal(a, b)
+    ref = gat_layer_forward_from_state(state, x, ei, H, True)
+    torch.testing.assert_close(a, ref, atol=ATOL, rtol=RTOL)
+    # the planes hold the row-major table's columns
+    wh_rm = torch.empty(n, H * F, device=dev())
+    rc = lib.gat_project(xd.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                         pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
+                         pp.c_dst.data_ptr(), H, F, wh_rm.data_ptr(), H * F, ss.data_ptr(), H,
+                         sd.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    sw = H * F // slices
+    planes = wh.view(slices, n, sw)
+    for g in range(slices):
+        assert torch.equal(planes[g], wh_rm[:, g * sw:(g + 1) * sw])
+
+
+def test_sliced_entry_points_reject_unsupported_shapes():
+    from atmlgraphattentionnetworks_amd import _lib
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    buf = torch.zeros(4096, device=dev())
+    p = buf.data_ptr()
+    # hf % slices != 0, slices < 2, plane width not a multiple of 4
+    assert lib.gat_edge_aggregate_sliced(p, p, 0, 0, 1, p, 1, 3, p, p, p, 2, 8, 0.2, p, p, 0,
+                                         st) == _lib.GAT_EINVAL
+    assert lib.gat_edge_aggregate_sliced(p, p, 0, 0, 1, p, 1, 1, p, p, p, 2, 8, 0.2, p, p, 0,
+                                         st) == _lib.GAT_EINVAL
+    assert lib.gat_project_sliced(p, 1, 4, p, p, p, p, p, p, 4, 2, 4, p, p, 4, p,
+                                  st) == _lib.GAT_EINVAL
+    # planes splitting a head (sw % f != 0) and a slope outside [0, 1]
+    assert lib.gat_edge_aggregate_sliced(p, p, 0, 0, 1, p, 1, 4, p, p, p, 2, 8, 0.2, p, p, 0,
+                                         st) == _lib.GAT_EUNSUPPORTED
+    assert lib.gat_edge_aggregate_sliced(p, p, 0, 0, 1, p, 1, 2, p, p, p, 2, 8, -0.5, p, p, 0,
+                                         st) == _lib.GAT_EUNSUPPORTED
+    # fin > 64 needs the pipelined projection: f a power of two <= 16, hf <= 64
+    assert lib.gat_project_sliced(p, 1, 100, p, p, p, p, p, p, 8, 12, 2, p, p, 8, p,
+                                  st) == _lib.GAT_EUNSUPPORTED

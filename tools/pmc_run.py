@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     args = ap.parse_args()
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
-    from atmlgraphattentionnetworks_amd.layer import alloc_table, edge_aggregate, project
+    from atmlgraphattentionnetworks_amd.layer import alloc_table, edge_aggregate, project, wh_slices
     from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
 
     dev = torch.device("cuda", 0)
@@ -42,14 +42,18 @@ def main():
     del ei
     with torch.no_grad():
         pp = layer.packed()
-        table, s_dst = project(x, pp, w.heads, w.out_channels)
+        slices = wh_slices(w.heads, w.out_channels, w.concat, layer.negative_slope,
+                           csr.num_edges // x.size(0))  # the layout the layer uses
+        table, s_dst = project(x, pp, w.heads, w.out_channels,
+                               table=alloc_table(x.size(0), w.heads, w.out_channels, dev,
+                                                 slices=slices))
         out = None
         for _ in range(args.iters):
             project(x, pp, w.heads, w.out_channels, table=table, s_dst=s_dst)
             out = edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat,
                                  layer.bias, out=out, pp=pp)
         torch.cuda.synchronize()
-    print(f"pmc_run done: {args.workload} N={x.size(0)} E'={csr.num_edges}")
+    print(f"pmc_run done: {args.workload} N={x.size(0)} E'={csr.num_edges} slices={slices}")
 
 
 if __name__ == "__main__":
