@@ -1136,7 +1136,7 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
-template <int G, int U, int V, bool FUSED>
+template <int G, int U, int V, bool FUSED, bool PIPE = false>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -1194,16 +1194,11 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     int cv[CL];
 #pragma unroll
     for (int t = 0; t < CL; ++t) cv[t] = col[min(e0 + c + t * G, e1 - 1)];
-    for (int k = e0; k < e1; k += U) {
-        const int nk = min(U, e1 - k);
-        int cn[CL];
-#pragma unroll
-        for (int t = 0; t < CL; ++t) cn[t] = col[min(k + U + c + t * G, e1 - 1)];
+    // gathers of one chunk: source ids broadcast from the group's col values
+    auto fetch = [&](const int (&cc)[CL], f32x4 (&v)[U][V], float (&s)[U]) {
         int j[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) j[u] = __shfl(cv[u / G], gbase + (u % G));
-        f32x4 v[U][V];
-        float s[U];
+        for (int u = 0; u < U; ++u) j[u] = __shfl(cc[u / G], gbase + (u % G));
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float* row = Whs + (size_t)j[u] * ld_wh;
@@ -1211,6 +1206,10 @@ __global__ __launch_bounds__(256) void k_edge_grp(
             for (int q = 0; q < V; ++q) v[u][q] = *reinterpret_cast<const f32x4*>(row + 4 * q);
             if constexpr (!FUSED) s[u] = Ss[(size_t)j[u] * ld_s + h];
         }
+    };
+    // scores, online softmax and accumulation of one gathered chunk
+    auto consume = [&](int k, f32x4 (&v)[U][V], float (&s)[U]) {
+        const int nk = min(U, e1 - k);
         if constexpr (FUSED) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -1288,8 +1287,45 @@ __global__ __launch_bounds__(256) void k_edge_grp(
             }
         }
         m = m_new;
+    };
+    if constexpr (PIPE) {
+        // gathers software-pipelined one chunk ahead too: chunk k+U's rows are
+        // in flight while chunk k is scored and accumulated (col two ahead)
+        f32x4 vc[U][V];
+        float sc[U];
+        fetch(cv, vc, sc);
+        int cn[CL];
 #pragma unroll
-        for (int t = 0; t < CL; ++t) cv[t] = cn[t];
+        for (int t = 0; t < CL; ++t) cn[t] = col[min(e0 + U + c + t * G, e1 - 1)];
+        for (int k = e0; k < e1; k += U) {
+            int cnn[CL];
+#pragma unroll
+            for (int t = 0; t < CL; ++t) cnn[t] = col[min(k + 2 * U + c + t * G, e1 - 1)];
+            f32x4 vn[U][V];
+            float sn[U];
+            if (k + U < e1) fetch(cn, vn, sn);
+            consume(k, vc, sc);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                sc[u] = sn[u];
+#pragma unroll
+                for (int q = 0; q < V; ++q) vc[u][q] = vn[u][q];
+            }
+#pragma unroll
+            for (int t = 0; t < CL; ++t) cn[t] = cnn[t];
+        }
+    } else {
+        for (int k = e0; k < e1; k += U) {
+            int cn[CL];
+#pragma unroll
+            for (int t = 0; t < CL; ++t) cn[t] = col[min(k + U + c + t * G, e1 - 1)];
+            f32x4 v[U][V];
+            float s[U];
+            fetch(cv, v, s);
+            consume(k, v, s);
+#pragma unroll
+            for (int t = 0; t < CL; ++t) cv[t] = cn[t];
+        }
     }
 
     const float inv = 1.f / (l + 1e-16f);
@@ -2379,6 +2415,24 @@ int gat_project_sliced(const float* x, int n, int fin, const float* w, const flo
                         heads * f / slices, s_src, ld_s, s_dst, stream);
 }
 
+}  // extern "C"
+
+// Fused lane-group edge kernel, optionally with the gathers pipelined one
+// chunk ahead (GAT_EDGE_PIPE A/B knob): instantiated for the (U, V) pairs the
+// default schedule uses.
+template <int G, int U, int V, class... A>
+static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A... a) {
+    if constexpr ((V == 1 && (U == 4 || U == 8)) || (V == 2 && (U == 8 || U == 16))) {
+        if (pipe) {
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true>), grid, block, 0, st, a...);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_edge_grp<G, U, V, true>), grid, block, 0, st, a...);
+}
+
+extern "C" {
+
 static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row_order,
                                int row_begin, int row_end, const float* wh, int ld_wh,
                                const float* s_src, int ld_s, const float* a_src,
@@ -2447,15 +2501,21 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
         const long long blocks = ((threads + 255) / 256) * nslices;
         if (blocks >= (1LL << 31)) return GAT_EUNSUPPORTED;
         const dim3 grid((unsigned)blocks), block(256);
-#define GAT_GRP_ARGS                                                                          \
-    grid, block, 0, st, rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s,    \
-        a_src, c_src, s_dst, heads, f, hf, concat, negative_slope, bias, out, ld_out, lse,     \
-        drop, y_heads, nslices, slice_w, slice_stride
+        // gathers pipelined one chunk ahead for long rows (U = 16, V = 2: one
+        // wave per SIMD at 360 registers, but 64 row gathers in flight per
+        // lane; tools/slice_probe.py, Reddit scale 2.60 -> 1.99 ms); shorter
+        // rows keep more, shallower waves (PPI 30.5 -> 32.9 us pipelined)
+        int pipe = (u == 16 && vv == 2) ? 1 : 0;
+        if (const char* ep = std::getenv("GAT_EDGE_PIPE")) pipe = std::atoi(ep);
+#define GAT_GRP_KARGS                                                                         \
+    rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,   \
+        heads, f, hf, concat, negative_slope, bias, out, ld_out, lse, drop, y_heads, nslices,  \
+        slice_w, slice_stride
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
     if (fused)                                                                        \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, true>), GAT_GRP_ARGS);              \
+        launch_edge_fused<G, UU, VV>(pipe, grid, block, st, GAT_GRP_KARGS);            \
     else                                                                              \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), GAT_GRP_ARGS)
+        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, GAT_GRP_KARGS)
 #define GAT_GRP_U(G, VV)                                                              \
     if (u == 4) { GAT_GRP_LAUNCH(G, 4, VV); }                                         \
     else if (u == 16) { GAT_GRP_LAUNCH(G, 16, VV); }                                  \
@@ -2477,7 +2537,7 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
 #undef GAT_GRP_G
 #undef GAT_GRP_U
 #undef GAT_GRP_LAUNCH
-#undef GAT_GRP_ARGS
+#undef GAT_GRP_KARGS
         return status_of(hipGetLastError());
     }
     const int lpe = next_pow2((round_up4(hf) + 3) / 4);

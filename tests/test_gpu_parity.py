@@ -42,13 +42,18 @@ VARIANTS = {
     "sliced8": {"GAT_WH_SLICES": "8"},
     "sliced8_v2": {"GAT_WH_SLICES": "8", "GAT_EDGE_V": "2"},
     "sliced4_proj_pipe": {"GAT_WH_SLICES": "4", "GAT_PROJ_WK_MAX": "0"},
+    # gathers pipelined one chunk ahead (default for U = 16, V = 2 only)
+    "pipe_u4": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "4"},
+    "pipe_u8_sliced2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "8", "GAT_WH_SLICES": "2"},
+    "pipe_u16_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
+    "nopipe_u16_v2": {"GAT_EDGE_PIPE": "0", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
 }
 
 
 @pytest.fixture(params=list(VARIANTS))
 def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
-              "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX"):
+              "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)

@@ -126,9 +126,13 @@ def test_backward_matches_oracle(case, kernel, monkeypatch):
 @pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[3], CASES[5]],
                          ids=["H8F8_cat", "H8F8_mean", "H1F7_mean", "H3F5_cat"])
 @pytest.mark.parametrize("p", [0.6, 0.2])
-@pytest.mark.parametrize("kernel", ["default", "stored"])
+@pytest.mark.parametrize("kernel", ["default", "stored", "fwd_pipe"])
 def test_dropout_forward_and_backward(case, p, kernel, monkeypatch):
-    if kernel != "default":
+    if kernel == "fwd_pipe":  # forward gathers pipelined one chunk ahead (U=16, V=2)
+        monkeypatch.setenv("GAT_EDGE_PIPE", "1")
+        monkeypatch.setenv("GAT_EDGE_U", "16")
+        monkeypatch.setenv("GAT_EDGE_V", "2")
+    elif kernel != "default":
         monkeypatch.setenv("GAT_BWD_KERNEL", kernel)
     n, e, fin, H, F, concat = case
     layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat, seed=3)
