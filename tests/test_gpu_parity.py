@@ -217,9 +217,10 @@ def test_ppi_shape_full_size_vs_oracle():
     torch.testing.assert_close(out, ref, atol=ATOL, rtol=RTOL)
 
 
-@pytest.mark.parametrize("slices,H,F,fin", [(8, 8, 8, 50), (4, 8, 8, 50), (2, 4, 8, 3),
-                                            (4, 4, 8, 128), (8, 8, 8, 602), (3, 3, 8, 20),
-                                            (4, 4, 16, 50)])
+@pytest.mark.parametrize("slices,H,F,fin", [(2, 8, 8, 50), (2, 8, 8, 602), (8, 8, 8, 50),
+                                            (4, 8, 8, 50), (2, 4, 8, 3), (4, 4, 8, 128),
+                                            (8, 8, 8, 602), (3, 3, 8, 20), (4, 4, 16, 50),
+                                            (2, 16, 4, 50), (2, 4, 16, 128)])
 def test_sliced_table_equals_row_major(slices, H, F, fin, monkeypatch):
     """gat_project_sliced + gat_edge_aggregate_sliced take this shape (status 0,
     checked directly) and give the row-major path's output bit for bit: the

@@ -92,6 +92,7 @@ def test_wh_slices_policy(monkeypatch):
     assert wh_slices(8, 8, True, -0.1, 28) == 1     # slope outside [0, 1]
     assert wh_slices(8, 6, True, 0.2, 28) == 1      # f % 4 != 0
     assert wh_slices(4, 12, True, 0.2, 28) == 1     # f/4 not a power of two
+    assert wh_slices(2, 16, True, 0.2, 28) == 1     # 128-B rows already
     monkeypatch.setenv("GAT_WH_SLICES", "8")
     assert wh_slices(8, 8, True, 0.2, 0) == 8
     assert wh_slices(6, 8, True, 0.2, 0) == 6
