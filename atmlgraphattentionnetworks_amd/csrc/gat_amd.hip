@@ -653,7 +653,7 @@ __global__ __launch_bounds__(256) void k_project_pipe(
                 for (int i = 0; i < 4; ++i) {
                     const int rr = rbase + i;
                     if (rr >= n) continue;
-                    Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
+                    if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
                     s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
                 }
             }
@@ -948,7 +948,7 @@ __global__ __launch_bounds__(256) void k_project_wk(
             v1 = fmaf(o[f], p1[f], v1);
             v2 = fmaf(o[f], p2[f], v2);
         }
-        Ss[(size_t)(row0 + r) * ld_s + h] = v1 + c1s[h];
+        if (Ss != nullptr) Ss[(size_t)(row0 + r) * ld_s + h] = v1 + c1s[h];
         s_dst[(size_t)(row0 + r) * H + h] = v2 + c2s[h];
     }
 }
@@ -2411,6 +2411,7 @@ int gat_project_sliced(const float* x, int n, int fin, const float* w, const flo
                        const float* c_dst, int heads, int f, int slices, float* wh,
                        float* s_src, int ld_s, float* s_dst, void* stream) {
     if (slices <= 0 || heads <= 0 || f <= 0 || (heads * f) % slices != 0) return GAT_EINVAL;
+    if (s_src == nullptr) ld_s = heads;  // the sliced edge kernel recomputes s_src
     return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
                         heads * f / slices, s_src, ld_s, s_dst, stream);
 }
@@ -2422,13 +2423,17 @@ int gat_project_sliced(const float* x, int n, int fin, const float* w, const flo
 // default schedule uses.
 template <int G, int U, int V, class... A>
 static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A... a) {
+    // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
+    // kernel — caps the blocks resident per CU (160 KB / bytes)
+    size_t lds = 0;
+    if (const char* el = std::getenv("GAT_EDGE_LDS")) lds = (size_t)std::atol(el);
     if constexpr ((V == 1 && (U == 4 || U == 8)) || (V == 2 && (U == 8 || U == 16))) {
         if (pipe) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true>), grid, block, 0, st, a...);
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true>), grid, block, lds, st, a...);
             return;
         }
     }
-    hipLaunchKernelGGL((k_edge_grp<G, U, V, true>), grid, block, 0, st, a...);
+    hipLaunchKernelGGL((k_edge_grp<G, U, V, true>), grid, block, lds, st, a...);
 }
 
 extern "C" {

@@ -346,23 +346,12 @@ def bench_distributed(args, metric: str):
         dist.all_reduce(e_blk)
         total_edges = float(e_blk.item())
 
-        # edge kernel alone on this rank's block (roofline), HIP events on its stream
-        from .layer import edge_aggregate, project
-        pp = layer.packed()
-        table, s_dst = project(x, pp, w.heads, w.out_channels)
-        out = edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat, layer.bias,
-                             pp=pp)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        stream = torch.cuda.current_stream()
-        ev0.record(stream)
-        for _ in range(args.edge_iters):
-            edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat, layer.bias,
-                           out=out, pp=pp)
-        ev1.record(stream)
-        ev1.synchronize()
-        edge_ms = ev0.elapsed_time(ev1) / args.edge_iters
+        # edge kernel alone on this rank's block (roofline), in the layer's table
+        # layout, HIP events on its stream
+        from bench import time_edge_kernel
+        edge_ms, slices = time_edge_kernel(layer, x, csr, args.edge_iters)
         n_block = x.size(0)
-        del x, ei, table, s_dst, out
+        del x, ei
 
         strong = []
         if not getattr(args, "no_strong_probe", False):
@@ -392,7 +381,7 @@ def bench_distributed(args, metric: str):
                                        "error": f"{type(exc).__name__}: {exc}"[:300]})
                     torch.cuda.empty_cache()
 
-    from bench import HBM_PEAK_GBS, edge_kernel_bytes, load_traffic  # noqa: E402
+    from bench import HBM_PEAK_GBS, edge_kernel_bytes, edge_kernel_name, load_traffic  # noqa: E402
     alg = edge_kernel_bytes(n_block, csr.num_edges, w.heads, w.out_channels, w.concat)
     ach = alg / (edge_ms * 1e-3) / 1e9
     res = None
@@ -411,7 +400,8 @@ def bench_distributed(args, metric: str):
                        "launch": launch},
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": load_traffic(args.workload),
-                         "kernel": "gat_edge_aggregate (rank 0 block)", "kernel_ms": edge_ms,
+                         "kernel": edge_kernel_name(slices) + " (rank 0 block)",
+                         "kernel_ms": edge_ms,
                          "algorithmic_bytes_per_launch": alg},
             "strong_scaling": {"graph": "one graph of the named workload's shape shared by "
                                         f"{world} ranks, node-range partitioned",

@@ -260,7 +260,7 @@ def gat_forward(x: torch.Tensor, csr: CSRGraph, pp: PackedParams, bias: torch.Te
         rc = lib.gat_project_sliced(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                     pp.a_src.data_ptr(), pp.c_src.data_ptr(),
                                     pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f, slices,
-                                    p_wh, p_ss, heads, p_sd, stream)
+                                    p_wh, 0, heads, p_sd, stream)
         if rc == 0:
             rc = lib.gat_edge_aggregate_sliced(
                 csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, p_wh, n, slices,

@@ -86,6 +86,41 @@ def cpu_baseline(layer_state, x, ei, heads, concat, n_edges_total, budget_s: flo
                        f"{threads} threads, {cpu_model()})")}
 
 
+def time_edge_kernel(layer, x, csr, iters: int):
+    """Mean launch time (ms) of the edge kernel the layer's eval forward uses,
+    on a node table in that forward's layout (layer.wh_slices), with HIP
+    events on the stream it is launched on.  Returns (ms, slices)."""
+    from atmlgraphattentionnetworks_amd.layer import (alloc_table, edge_aggregate, project,
+                                                      wh_slices)
+    n = x.size(0)
+    heads, f = layer.num_heads, layer.output_channels
+    pp = layer.packed()
+    slices = wh_slices(heads, f, layer.concat, layer.negative_slope,
+                       csr.num_edges // max(n, 1))
+    table, s_dst = project(x, pp, heads, f,
+                           table=alloc_table(n, heads, f, x.device, slices=slices))
+    out = torch.empty(n, heads * f if layer.concat else f, device=x.device)
+
+    def run():
+        edge_aggregate(csr, table, s_dst, heads, f, layer.concat, layer.bias, out=out, pp=pp)
+
+    for _ in range(5):
+        run()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(iters):
+        run()
+    ev1.record(stream)
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) / iters, slices
+
+
+def edge_kernel_name(slices: int) -> str:
+    return ("gat_edge_aggregate_sliced (k_edge_grp, %d column planes)" % slices if slices > 1
+            else "gat_edge_aggregate (k_edge_grp)")
+
+
 def train_step(layer, x, ei, n_edges: int, steps: int) -> dict:
     """One training step of the layer: forward in training
     mode with the layer's attention dropout (0.6, GAT.py:61) and the HIP
@@ -185,7 +220,7 @@ def main():
         return bench_distributed(args, METRIC)
 
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
-    from atmlgraphattentionnetworks_amd.layer import alloc_table, edge_aggregate, project, wh_slices
+    from atmlgraphattentionnetworks_amd.layer import project
     from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
 
     dev = torch.device("cuda", 0)
@@ -234,27 +269,12 @@ def main():
         elapsed = time.perf_counter() - t0
         ms_per_step = elapsed * 1e3 / args.steps
 
-        # edge kernel alone, HIP events on the stream it is launched on
+        # edge kernel alone, in the layer's table layout, HIP events on its stream
+        edge_ms, slices = time_edge_kernel(layer, x, csr, args.edge_iters)
         pp = layer.packed()
-        # the table layout the layer's forward uses (layer.wh_slices)
-        slices = wh_slices(w.heads, w.out_channels, w.concat, layer.negative_slope,
-                           n_edges // max(n, 1))
-        table, s_dst = project(x, pp, w.heads, w.out_channels,
-                               table=alloc_table(n, w.heads, w.out_channels, dev, slices=slices))
-        out = torch.empty(n, w.heads * w.out_channels if w.concat else w.out_channels,
-                          device=dev)
-        for _ in range(5):
-            edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat, layer.bias,
-                           out=out, pp=pp)
+        table, s_dst = project(x, pp, w.heads, w.out_channels)
         stream = torch.cuda.current_stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record(stream)
-        for _ in range(args.edge_iters):
-            edge_aggregate(csr, table, s_dst, w.heads, w.out_channels, w.concat, layer.bias,
-                           out=out, pp=pp)
-        ev1.record(stream)
-        ev1.synchronize()
-        edge_ms = ev0.elapsed_time(ev1) / args.edge_iters
         # projection alone: short kernel, so time launches captured in a graph
         gp = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gp):
@@ -292,8 +312,7 @@ def main():
                    "parallelism": "single GPU", "launch": "hipGraph" if graph else "eager"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("gat_edge_aggregate_sliced (k_edge_grp, %d column planes)" % slices
-                                if slices > 1 else "gat_edge_aggregate (k_edge_grp)"),
+                     "kernel": edge_kernel_name(slices),
                      "kernel_ms": edge_ms,
                      "algorithmic_bytes_per_launch": alg_bytes},
         "breakdown_ms": {"project": proj_ms, "edge": edge_ms, "csr_build_once": csr_ms},

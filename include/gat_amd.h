@@ -127,7 +127,8 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
  * Results equal the row-major entry points' (same arithmetic, same order).
  *
  * gat_project_sliced: as gat_project with ld_wh = sw (heads*f % slices == 0,
- *   sw % 4 == 0); n_table = n.  GAT_EUNSUPPORTED for shapes whose projection
+ *   sw % 4 == 0); n_table = n.  s_src may be NULL (not written: the sliced
+ *   edge kernel recomputes it).  GAT_EUNSUPPORTED for shapes whose projection
  *   kernel writes row-major only (fin > 64 needs f a power of two <= 16 and
  *   heads*f <= 64).
  * gat_edge_aggregate_sliced: concat only, LeakyReLU slope in [0, 1], sw % f == 0

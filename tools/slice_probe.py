@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--vs", default="1,2")
     ap.add_argument("--us", default="")
     ap.add_argument("--pipes", default="0", help="GAT_EDGE_PIPE values (0 = default)")
+    ap.add_argument("--lds", default="0", help="GAT_EDGE_LDS values (0 = none)")
     args = ap.parse_args()
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer, _lib, get_csr
     from atmlgraphattentionnetworks_amd.layer import gat_forward
@@ -93,7 +94,8 @@ def main():
     vs = [int(v) for v in args.vs.split(",")]
     us = [int(v) for v in args.us.split(",")] if args.us else [0]
     occs = [int(v) for v in args.pipes.split(",")]
-    variants = [(s, v, u, o) for s in slices for v in vs for u in us for o in occs]
+    ldss = [int(v) for v in args.lds.split(",")]
+    variants = [(s, v, u, o, d) for s in slices for v in vs for u in us for o in occs for d in ldss]
     res = {k: [] for k in variants}
     pres = {s: [] for s in slices}
     fres = {s: [] for s in slices}
@@ -105,7 +107,8 @@ def main():
             proj()
             prepared[s] = (wh, sd, proj)
         for _ in range(args.rounds):
-            for (s, v, u, o) in variants:
+            for (s, v, u, o, d) in variants:
+                os.environ["GAT_EDGE_LDS"] = str(d)
                 os.environ["GAT_EDGE_V"] = str(v)
                 os.environ["GAT_EDGE_PIPE"] = str(o)
                 if u:
@@ -114,11 +117,12 @@ def main():
                     os.environ.pop("GAT_EDGE_U", None)
                 wh, sd, _ = prepared[s]
                 out = torch.empty(n, hf, device=dev)
-                res[(s, v, u, o)].append(time_fn(edge_fn(s, wh, sd, out), args.iters))
-                outs[(s, v, u, o)] = out
+                res[(s, v, u, o, d)].append(time_fn(edge_fn(s, wh, sd, out), args.iters))
+                outs[(s, v, u, o, d)] = out
             os.environ.pop("GAT_EDGE_V", None)
             os.environ.pop("GAT_EDGE_U", None)
             os.environ.pop("GAT_EDGE_PIPE", None)
+            os.environ.pop("GAT_EDGE_LDS", None)
             for s in slices:
                 pres[s].append(time_fn(prepared[s][2], args.iters))
                 os.environ["GAT_WH_SLICES"] = str(s)
@@ -130,7 +134,7 @@ def main():
     summary = {}
     for k, ts in res.items():
         med = statistics.median(ts)
-        summary[f"edge_s{k[0]}_v{k[1]}_u{k[2]}_pipe{k[3]}"] = {
+        summary[f"edge_s{k[0]}_v{k[1]}_u{k[2]}_pipe{k[3]}_lds{k[4]}"] = {
             "median_ms": round(med, 5), "min_ms": round(min(ts), 5),
             "GBps_alg": round(alg / med / 1e6, 1),
             "max_abs_diff": float((outs[k] - ref).abs().max())}
