@@ -2749,6 +2749,13 @@ int gat_bwd_table_layout(int heads, int f, int concat, int* ld_t) {
 
 // edges per chunk of the recompute backward kernels: the forward's thresholds;
 // GAT_BWD_U overrides (A/B knob)
+// GAT_BWD_LDS (A/B knob): dynamic LDS bytes per block for the recompute
+// backward kernels, unused by them — caps the blocks resident per CU
+static size_t bwd_lds_bytes() {
+    const char* v = std::getenv("GAT_BWD_LDS");
+    return v != nullptr ? (size_t)std::atol(v) : 0;
+}
+
 static int bwd_unroll(int hint) {
     int u = hint <= 0 ? 8 : hint <= 32 ? 4 : hint <= 64 ? 8 : 16;
     if (const char* v = std::getenv("GAT_BWD_U")) {
@@ -2790,8 +2797,9 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
     int u = bwd_unroll(edges_per_row_hint);
     const long long threads = (long long)rows * g;
     const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+    const size_t bwd_lds = bwd_lds_bytes();
 #define GAT_BT(G, UU)                                                                         \
-    hipLaunchKernelGGL((k_bwd_targets<G, UU>), grid, block, 0, st, rowptr, col, row_order,    \
+    hipLaunchKernelGGL((k_bwd_targets<G, UU>), grid, block, bwd_lds, st, rowptr, col, row_order,    \
                        row_begin, row_end, wh, ld_wh, a_src, c_src, s_dst, lse, y_heads,      \
                        grad_out, heads, f, hf, concat, negative_slope, drop, ds_dst, table,   \
                        ld_t)
@@ -2841,8 +2849,9 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
     const int g = next_pow2(hf / 4);
     int u = bwd_unroll(edges_per_row_hint);
     const dim3 grid(num_parts / 4), block(256);
+    const size_t bwd_lds = bwd_lds_bytes();
 #define GAT_BS(G, UU)                                                                         \
-    hipLaunchKernelGGL((k_bwd_sources<G, UU>), grid, block, 0, st, csc_ptr, csc_dst, csc_eid,  \
+    hipLaunchKernelGGL((k_bwd_sources<G, UU>), grid, block, bwd_lds, st, csc_ptr, csc_dst, csc_eid,  \
                        num_nodes, wh, ld_wh, table, ld_t, ds_dst, a_src, c_src, a_dst, heads, \
                        f, hf, concat, negative_slope, drop, dwh, ld_dwh, partials)
 #define GAT_BS_U(G)                      \
