@@ -40,8 +40,8 @@ SIGNATURES = {
                                     _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
                                     _c_float, _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_project_sliced": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
-                                    _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_int, _c_vp,
-                                    _c_vp]),
+                                    _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_int,
+                                    _c_vp, _c_vp]),
     "gat_edge_aggregate_sliced": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
                                            _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_float,
                                            _c_vp, _c_vp, _c_int, _c_vp]),

@@ -2254,7 +2254,7 @@ int gat_table_layout(int heads, int f, int* ld, int* s_off) {
 static int project_impl(const float* x, int n, int fin, const float* w, const float* b,
                         const float* a_src, const float* c_src, const float* a_dst,
                         const float* c_dst, int heads, int f, int slices, float* wh, int ld_wh,
-                        float* s_src, int ld_s, float* s_dst, void* stream) {
+                        float* s_src, int ld_s, float* s_dst, void* stream, int n_table = 0) {
     if (n < 0 || fin < 0 || heads <= 0 || f <= 0 || slices <= 0) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
@@ -2265,9 +2265,10 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     } else if (ld_wh < round_up4(hf) || (ld_wh & 3) || ld_s < heads) {
         return GAT_EINVAL;
     }
+    if (sliced && n_table < n) return GAT_EINVAL;
     if (n == 0) return GAT_OK;
     const int slice_w = sliced ? ld_wh : round_up4(hf);
-    const long long slice_stride = sliced ? (long long)n * ld_wh : 0;
+    const long long slice_stride = sliced ? (long long)n_table * ld_wh : 0;
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
     const int nt = (hf + 15) / 16;
@@ -2408,12 +2409,12 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
 
 int gat_project_sliced(const float* x, int n, int fin, const float* w, const float* b,
                        const float* a_src, const float* c_src, const float* a_dst,
-                       const float* c_dst, int heads, int f, int slices, float* wh,
+                       const float* c_dst, int heads, int f, int slices, float* wh, int n_table,
                        float* s_src, int ld_s, float* s_dst, void* stream) {
     if (slices <= 0 || heads <= 0 || f <= 0 || (heads * f) % slices != 0) return GAT_EINVAL;
     if (s_src == nullptr) ld_s = heads;  // the sliced edge kernel recomputes s_src
     return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
-                        heads * f / slices, s_src, ld_s, s_dst, stream);
+                        heads * f / slices, s_src, ld_s, s_dst, stream, n_table);
 }
 
 }  // extern "C"

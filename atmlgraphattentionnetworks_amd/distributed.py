@@ -76,8 +76,10 @@ class HipOps:
     """The HIP kernels (default)."""
 
     @staticmethod
-    def alloc_table(n, heads, f, device, packed=True, wh_only=False):
+    def alloc_table(n, heads, f, device, packed=True, wh_only=False, slices=1):
         from .layer import alloc_table
+        if slices > 1:
+            return alloc_table(n, heads, f, device, slices=slices)
         return alloc_table(n, heads, f, device, packed=packed, wh_only=wh_only)
 
     @staticmethod
@@ -138,10 +140,20 @@ class ShardedGAT:
         # [Wh | s_src] row is 288 B and every gather straddles an extra line).
         # Otherwise one packed buffer [Wh | s_src].  replicate: the default
         # separate layout (no collective to feed).
+        # Wh-only tables can also be sliced into column planes (layer.wh_slices,
+        # the single-GPU eval forward's layout): one all-gather per plane.
         hl = self.f // 4
         self.wh_only = (exchange == "allgather" and self.f % 4 == 0 and hl > 0 and
                         (hl & (hl - 1)) == 0 and _default_score(layer))
+        self.slices = 1
         if self.wh_only:
+            from .layer import wh_slices
+            self.slices = wh_slices(self.heads, self.f, self.concat, 0.2,
+                                    csr.num_edges // max(csr.num_nodes, 1))
+        if self.wh_only and self.slices > 1:
+            self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev,
+                                              slices=self.slices)
+        elif self.wh_only:
             self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev, wh_only=True)
         else:
             self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev,
@@ -163,9 +175,13 @@ class ShardedGAT:
     def phase_exchange(self):
         if self.exchange == "allgather" and self.world > 1:
             m = self.rows_per_part
-            buf = self.table.buf
-            dist.all_gather_into_tensor(buf, buf[self.rank * m:(self.rank + 1) * m],
-                                        group=self.group)
+            # one in-place all-gather per column plane (a single one for the
+            # row-major table)
+            planes = [self.table.buf[g] for g in range(self.slices)] if self.slices > 1 \
+                else [self.table.buf]
+            for buf in planes:
+                dist.all_gather_into_tensor(buf, buf[self.rank * m:(self.rank + 1) * m],
+                                            group=self.group)
 
     def phase_edges(self):
         s_dst = self.s_dst_full if self.exchange == "allgather" else \
@@ -180,7 +196,9 @@ class ShardedGAT:
         return self.phase_edges()
 
     def local_x(self, x_full):
-        return x_full[self.r0:self.r1].contiguous() if self.exchange == "allgather" else x_full
+        # a fresh copy: a row view of x can start off a 16-B boundary, which the
+        # whole-K projection (the one that writes the sliced table) needs
+        return x_full[self.r0:self.r1].clone() if self.exchange == "allgather" else x_full
 
 
 def gather_output(local_out: torch.Tensor, bounds: List[int], group=None) -> torch.Tensor:

@@ -20,7 +20,9 @@ No PyG import, no CPU path: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import itertools
 import os
+import weakref
 from typing import NamedTuple, Optional, Tuple
 
 import torch
@@ -76,6 +78,28 @@ def pack_params(layer: "GraphAttentionLayer", cached: Optional[PackedParams] = N
     return PackedParams(w, b, a_src, c_src, a_dst, c_dst, key)
 
 
+# Packed-buffer invalidation without walking the 6H parameters per forward
+# (that walk cost ~16 us of host time per call).  Each per-head Linear carries
+# its layer's token; a global parameter-registration hook marks the layer
+# stale when one of them gets a new Parameter (setattr, load_state_dict with
+# assign=True).  packed() also checks that the first head's parameters still
+# alias the packed buffers, which catches .to()/deepcopy-style re-storage.
+_owners: "weakref.WeakValueDictionary[int, torch.nn.Module]" = weakref.WeakValueDictionary()
+_tokens = itertools.count(1)
+
+
+def _mark_owner_dirty(module, name, param):
+    token = module.__dict__.get("_gat_owner")
+    if token is not None:
+        owner = _owners.get(token)
+        if owner is not None:
+            owner.__dict__["_packed_dirty"] = True
+    return None
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_mark_owner_dirty)
+
+
 def _stream(device: torch.device) -> int:
     """Raw hipStream_t of torch's current stream on ``device``."""
     return torch._C._cuda_getCurrentRawStream(device.index)
@@ -92,7 +116,9 @@ class NodeTable(NamedTuple):
     edge kernel recomputes s_src from the gathered Wh row (the library then
     refuses, rather than guesses, if it would need s_src).
     Sliced layout (``slices > 1``): Wh as ``slices`` column planes
-    [slices, N, ld_wh = H*F/slices] (gat_project_sliced / gat_edge_aggregate_sliced)."""
+    [slices, N, ld_wh = H*F/slices] (gat_project_sliced / gat_edge_aggregate_sliced);
+    no s_src (the sliced edge kernel recomputes it).  ``rows`` views keep the
+    plane stride (``wh.stride(0)``), so a rank can project into its slot."""
     wh: torch.Tensor
     ld_wh: int
     s_src: Optional[torch.Tensor]
@@ -103,7 +129,8 @@ class NodeTable(NamedTuple):
     def rows(self, start: int, stop: int) -> "NodeTable":
         """The table restricted to rows [start, stop) (views, same strides)."""
         if self.slices > 1:
-            raise ValueError("row views of a sliced node table are not supported")
+            return NodeTable(self.wh[:, start:stop], self.ld_wh, None, self.ld_s, None,
+                             self.slices)
         return NodeTable(self.wh[start:stop], self.ld_wh,
                          None if self.s_src is None else self.s_src[start:stop], self.ld_s,
                          None if self.buf is None else self.buf[start:stop])
@@ -112,12 +139,11 @@ class NodeTable(NamedTuple):
 def alloc_table(n: int, heads: int, f: int, device, packed: bool = False,
                 wh_only: bool = False, slices: int = 1) -> NodeTable:
     if slices > 1:
-        if packed or wh_only or (heads * f) % slices:
-            raise ValueError("a sliced table is Wh planes plus a compact s_src")
+        if packed or (heads * f) % slices:
+            raise ValueError("a sliced table is Wh planes only")
         sw = heads * f // slices
-        wh = torch.empty(slices, n, sw, dtype=torch.float32, device=device)
-        s_src = torch.empty(n, heads, dtype=torch.float32, device=device)
-        return NodeTable(wh, sw, s_src, heads, None, slices)
+        wh = torch.zeros(slices, n, sw, dtype=torch.float32, device=device)
+        return NodeTable(wh, sw, None, heads, wh, slices)
     if wh_only:
         hfp = (heads * f + 3) // 4 * 4
         buf = torch.zeros(n, hfp, dtype=torch.float32, device=device)
@@ -141,16 +167,17 @@ def project(x: torch.Tensor, pp: PackedParams, heads: int, f: int,
         table = alloc_table(n, heads, f, x.device)
     if s_dst is None:
         s_dst = torch.empty(n, heads, dtype=torch.float32, device=x.device)
-    s_src = table.s_src
-    if s_src is None:  # Wh-only table: the scores still have to go somewhere
-        s_src = torch.empty(n, heads, dtype=torch.float32, device=x.device)
     if table.slices > 1:
+        # planes of wh.stride(0) / ld_wh rows; wh may be a rank's slot (rows view)
         _lib.check(lib.gat_project_sliced(
             x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(),
             pp.c_src.data_ptr(), pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
-            table.slices, table.wh.data_ptr(), s_src.data_ptr(), table.ld_s, s_dst.data_ptr(),
-            _stream(x.device)), "gat_project_sliced")
+            table.slices, table.wh.data_ptr(), table.wh.stride(0) // table.ld_wh, 0, heads,
+            s_dst.data_ptr(), _stream(x.device)), "gat_project_sliced")
         return table, s_dst
+    s_src = table.s_src
+    if s_src is None:  # Wh-only table: the scores still have to go somewhere
+        s_src = torch.empty(n, heads, dtype=torch.float32, device=x.device)
     _lib.check(lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
                                pp.c_dst.data_ptr(), heads, f, table.wh.data_ptr(), table.ld_wh,
@@ -181,7 +208,7 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
             raise ValueError("the sliced edge kernel recomputes s_src (pp) and has no lse")
         _lib.check(lib.gat_edge_aggregate_sliced(
             csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
-            row_begin, rows, table.wh.data_ptr(), table.wh.size(1), table.slices,
+            row_begin, rows, table.wh.data_ptr(), table.wh.stride(0) // table.ld_wh, table.slices,
             pp.a_src.data_ptr(), pp.c_src.data_ptr(), s_dst.data_ptr(), heads, f,
             float(negative_slope), bias.data_ptr(), out.data_ptr(), hint,
             _stream(table.wh.device)), "gat_edge_aggregate_sliced")
@@ -260,7 +287,7 @@ def gat_forward(x: torch.Tensor, csr: CSRGraph, pp: PackedParams, bias: torch.Te
         rc = lib.gat_project_sliced(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                     pp.a_src.data_ptr(), pp.c_src.data_ptr(),
                                     pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f, slices,
-                                    p_wh, 0, heads, p_sd, stream)
+                                    p_wh, n, 0, heads, p_sd, stream)
         if rc == 0:
             rc = lib.gat_edge_aggregate_sliced(
                 csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, p_wh, n, slices,
@@ -390,7 +417,31 @@ class GraphAttentionLayer(torch.nn.Module):
             params[5 * H + h].data = c_dst[h:h + 1]
         self._packed = PackedParams(w, b, a_src, c_src, a_dst, c_dst,
                                     tuple(p.data_ptr() for p in params))
+        token = self.__dict__.get("_gat_token")
+        if token is None or _owners.get(token) is not self:
+            token = next(_tokens)
+            self.__dict__["_gat_token"] = token
+            _owners[token] = self
+        for mods in (self.ws, self.attentions1, self.attentions2):
+            for m in mods._modules.values():
+                m.__dict__["_gat_owner"] = token
+        self.__dict__["_packed_dirty"] = False
         return self._packed
+
+    def _packed_aliases(self, pp: PackedParams) -> bool:
+        """Head 0's six parameters still start the six packed buffers."""
+        mods = self._modules
+        if not mods["ws"]._modules:
+            return True
+        p0 = mods["ws"]._modules["0"]._parameters
+        p1 = mods["attentions1"]._modules["0"]._parameters
+        p2 = mods["attentions2"]._modules["0"]._parameters
+        return (p0["weight"].data_ptr() == pp.w.data_ptr()
+                and p0["bias"].data_ptr() == pp.b.data_ptr()
+                and p1["weight"].data_ptr() == pp.a_src.data_ptr()
+                and p1["bias"].data_ptr() == pp.c_src.data_ptr()
+                and p2["weight"].data_ptr() == pp.a_dst.data_ptr()
+                and p2["bias"].data_ptr() == pp.c_dst.data_ptr())
 
     def _apply(self, fn, recurse=True):
         # .to() / .cuda() / .float() replace each parameter's storage: re-pack
@@ -399,9 +450,13 @@ class GraphAttentionLayer(torch.nn.Module):
         return out
 
     def packed(self) -> PackedParams:
-        """The packed parameter buffers (re-bound if a parameter was replaced)."""
+        """The packed parameter buffers, re-bound if a parameter was replaced
+        (registration hook) or re-stored (head 0 no longer aliases them).  A
+        ``.data`` reassignment of a later head's parameter is not detected:
+        call ``_bind_packed()`` after one."""
         pp = self._packed
-        if pp is None or pp.key != tuple(p.data_ptr() for p in _param_list(self)):
+        if pp is None or self.__dict__.get("_packed_dirty", True) or \
+                not self._packed_aliases(pp):
             pp = self._bind_packed()
         if pp.w.dtype != torch.float32:
             raise ValueError(f"parameters must be float32 (the reference's dtype), got {pp.w.dtype}")

@@ -127,8 +127,10 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
  * Results equal the row-major entry points' (same arithmetic, same order).
  *
  * gat_project_sliced: as gat_project with ld_wh = sw (heads*f % slices == 0,
- *   sw % 4 == 0); n_table = n.  s_src may be NULL (not written: the sliced
- *   edge kernel recomputes it).  GAT_EUNSUPPORTED for shapes whose projection
+ *   sw % 4 == 0), writing rows [0, n) of planes of n_table >= n rows (wh may
+ *   point at row r0 of the first plane: a rank's slot of a table the
+ *   multi-GPU path all-gathers plane by plane).  s_src may be NULL (not
+ *   written: the sliced edge kernel recomputes it).  GAT_EUNSUPPORTED for shapes whose projection
  *   kernel writes row-major only (fin > 64 needs f a power of two <= 16 and
  *   heads*f <= 64).
  * gat_edge_aggregate_sliced: concat only, LeakyReLU slope in [0, 1], sw % f == 0
@@ -138,7 +140,7 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
  */
 int gat_project_sliced(const float* x, int n, int fin, const float* w, const float* b,
                        const float* a_src, const float* c_src, const float* a_dst,
-                       const float* c_dst, int heads, int f, int slices, float* wh,
+                       const float* c_dst, int heads, int f, int slices, float* wh, int n_table,
                        float* s_src, int ld_s, float* s_dst, void* stream);
 int gat_edge_aggregate_sliced(const int* rowptr, const int* col, const int* row_order,
                               int row_begin, int row_end, const float* wh, int n_table,

@@ -21,8 +21,10 @@ class CpuOps:
     same packed table layout the HIP path uses."""
 
     @staticmethod
-    def alloc_table(n, heads, f, device, packed=True, wh_only=False):
+    def alloc_table(n, heads, f, device, packed=True, wh_only=False, slices=1):
         from atmlgraphattentionnetworks_amd.layer import alloc_table
+        if slices > 1:
+            return alloc_table(n, heads, f, device, slices=slices)
         if wh_only or packed:
             return alloc_table(n, heads, f, device, packed=packed, wh_only=wh_only)
         hf = heads * f
@@ -32,10 +34,21 @@ class CpuOps:
         return NodeTable(wh, wh.size(1), s_src, heads)
 
     @staticmethod
+    def _row_major(table):
+        """[n, hf] view of the table's Wh (a copy for the sliced planes)."""
+        if table.slices > 1:
+            s, n, sw = table.wh.shape
+            return table.wh.permute(1, 0, 2).reshape(n, s * sw)
+        return table.wh
+
+    @staticmethod
     def project(x, pp, heads, f, table, s_dst):
         hf = heads * f
         wh = x @ pp.w.T + pp.b
-        table.wh[:, :hf] = wh
+        if table.slices > 1:  # plane g holds columns [g*sw, (g+1)*sw)
+            table.wh[:] = wh.view(wh.size(0), table.slices, -1).permute(1, 0, 2)
+        else:
+            table.wh[:, :hf] = wh
         v = wh.view(-1, heads, f)
         if table.s_src is not None:
             table.s_src[:, :heads] = (v * pp.a_src.view(heads, f)).sum(-1) + pp.c_src
@@ -48,9 +61,10 @@ class CpuOps:
         deg = rp[1:] - rp[:-1]
         dst = torch.repeat_interleave(torch.arange(csr.num_nodes), deg)
         src = csr.col.long()
+        whf = CpuOps._row_major(table)
         if table.s_src is None:  # Wh-only table: recompute s_src from the Wh rows (fused score)
             assert pp is not None
-            s_src = (table.wh[:, :hf].view(-1, heads, f) * pp.a_src.view(heads, f)).sum(-1) \
+            s_src = (whf[:, :hf].view(-1, heads, f) * pp.a_src.view(heads, f)).sum(-1) \
                 + pp.c_src
         else:
             s_src = table.s_src[:, :heads]
@@ -60,7 +74,7 @@ class CpuOps:
         p = (e - m[dst]).exp()
         l = torch.zeros(csr.num_nodes, heads).index_add_(0, dst, p)
         a = p / (l[dst] + 1e-16)
-        msg = table.wh[src, :hf].view(-1, heads, f) * a.unsqueeze(-1)
+        msg = whf[src, :hf].view(-1, heads, f) * a.unsqueeze(-1)
         y = torch.zeros(csr.num_nodes, heads, f).index_add_(0, dst, msg)
         out[:] = (y.reshape(csr.num_nodes, hf) if concat else y.mean(1)) + bias
         return out
@@ -108,8 +122,10 @@ def _cpu_csr(ei, n):
                     torch.from_numpy(s[order].astype(np.int32)), n, len(s))
 
 
-def _worker(rank, world, port, exchange, concat, results, F=8):
+def _worker(rank, world, port, exchange, concat, results, F=8, slices=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if slices is not None:
+        os.environ["GAT_WH_SLICES"] = str(slices)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from atmlgraphattentionnetworks_amd.distributed import ShardedGAT, gather_output
@@ -119,6 +135,7 @@ def _worker(rank, world, port, exchange, concat, results, F=8):
         sh = ShardedGAT(_Layer(state, H, F, concat), csr, world, rank, exchange=exchange,
                         ops=CpuOps)
         results["wh_only"] = sh.wh_only
+        results["slices"] = sh.slices
         out = sh.forward(sh.local_x(x))
         full = gather_output(out, sh.bounds)
         if rank == 0:
@@ -155,6 +172,19 @@ def test_sharded_forward_matches_oracle(world, exchange, concat, F):
     # edge-balanced: every rank within 10% of E'/P
     edges = results["edges"]
     assert max(edges) <= 1.1 * sum(edges) / world + 50, edges
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_forward_sliced_table(world):
+    """The Wh-only table as 2 column planes (the layout the single-GPU eval
+    forward uses at >= 16 edges per row): one in-place all-gather per plane."""
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), "allgather", True, results, 8, 2),
+             nprocs=world, join=True)
+    assert results["wh_only"] and results["slices"] == 2
+    assert results["shape_ok"]
+    assert results["max_diff"] < 1e-5, results["max_diff"]
 
 
 def test_partition_rows_edge_balanced():

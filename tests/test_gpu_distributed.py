@@ -14,7 +14,14 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("P", [2, 4, 8])
 @pytest.mark.parametrize("exchange", ["allgather", "replicate"])
 @pytest.mark.parametrize("concat", [True, False])
-def test_sharded_hip_path_matches_single_gpu(P, exchange, concat):
+@pytest.mark.parametrize("table", ["default", "row_major"])
+def test_sharded_hip_path_matches_single_gpu(P, exchange, concat, table, monkeypatch):
+    """table=default: at 21 edges per row the concat all-gather table is 2
+    column planes (one all-gather per plane); row_major: GAT_WH_SLICES=1."""
+    if table == "row_major":
+        monkeypatch.setenv("GAT_WH_SLICES", "1")
+    else:
+        monkeypatch.delenv("GAT_WH_SLICES", raising=False)
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
     from atmlgraphattentionnetworks_amd.distributed import ShardedGAT
     from atmlgraphattentionnetworks_amd.synthetic import uniform_graph
@@ -32,6 +39,8 @@ def test_sharded_hip_path_matches_single_gpu(P, exchange, concat):
     csr = get_csr(ei, n)
     with torch.no_grad():
         ranks = [ShardedGAT(layer, csr, P, r, exchange=exchange) for r in range(P)]
+        if exchange == "allgather":
+            assert ranks[0].slices == (2 if concat and table == "default" else 1)
         for sh in ranks:
             sh.phase_project(sh.local_x(x))
         if exchange == "allgather":
@@ -39,7 +48,10 @@ def test_sharded_hip_path_matches_single_gpu(P, exchange, concat):
             for dst in ranks:
                 for src in ranks:
                     sl = slice(src.rank * m, (src.rank + 1) * m)
-                    dst.table.buf[sl] = src.table.buf[sl]
+                    if dst.slices > 1:  # [planes, rows, plane width]
+                        dst.table.buf[:, sl] = src.table.buf[:, sl]
+                    else:
+                        dst.table.buf[sl] = src.table.buf[sl]
         outs = [sh.phase_edges().clone() for sh in ranks]
     full = torch.cat(outs).cpu()
     ref = gat_layer_forward_from_state(state, x.cpu(), ei.cpu(), H, concat)

@@ -240,8 +240,9 @@ def test_sliced_table_equals_row_major(slices, H, F, fin, monkeypatch):
     lib = _lib.load()
     rc = lib.gat_project_sliced(xd.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                 pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                                pp.c_dst.data_ptr(), H, F, slices, wh.data_ptr(), ss.data_ptr(),
-                                H, sd.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                                pp.c_dst.data_ptr(), H, F, slices, wh.data_ptr(), n,
+                                ss.data_ptr(), H, sd.data_ptr(),
+                                torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     a = run_layer(layer, x, ei)
     monkeypatch.setenv("GAT_WH_SLICES", "1")
@@ -273,7 +274,10 @@ def test_sliced_entry_points_reject_unsupported_shapes():
                                          st) == _lib.GAT_EINVAL
     assert lib.gat_edge_aggregate_sliced(p, p, 0, 0, 1, p, 1, 1, p, p, p, 2, 8, 0.2, p, p, 0,
                                          st) == _lib.GAT_EINVAL
-    assert lib.gat_project_sliced(p, 1, 4, p, p, p, p, p, p, 4, 2, 4, p, p, 4, p,
+    assert lib.gat_project_sliced(p, 1, 4, p, p, p, p, p, p, 4, 2, 4, p, 1, p, 4, p,
+                                  st) == _lib.GAT_EINVAL
+    # planes shorter than the rows written
+    assert lib.gat_project_sliced(p, 8, 4, p, p, p, p, p, p, 8, 8, 2, p, 4, p, 8, p,
                                   st) == _lib.GAT_EINVAL
     # planes splitting a head (sw % f != 0) and a slope outside [0, 1]
     assert lib.gat_edge_aggregate_sliced(p, p, 0, 0, 1, p, 1, 4, p, p, p, 2, 8, 0.2, p, p, 0,
@@ -281,5 +285,5 @@ def test_sliced_entry_points_reject_unsupported_shapes():
     assert lib.gat_edge_aggregate_sliced(p, p, 0, 0, 1, p, 1, 2, p, p, p, 2, 8, -0.5, p, p, 0,
                                          st) == _lib.GAT_EUNSUPPORTED
     # fin > 64 needs the pipelined projection: f a power of two <= 16, hf <= 64
-    assert lib.gat_project_sliced(p, 1, 100, p, p, p, p, p, p, 8, 12, 2, p, p, 8, p,
+    assert lib.gat_project_sliced(p, 1, 100, p, p, p, p, p, p, 8, 12, 2, p, 1, p, 8, p,
                                   st) == _lib.GAT_EUNSUPPORTED

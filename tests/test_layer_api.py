@@ -99,3 +99,33 @@ def test_wh_slices_policy(monkeypatch):
     assert wh_slices(4, 8, True, 0.2, 0) == 4
     monkeypatch.setenv("GAT_WH_SLICES", "1")
     assert wh_slices(8, 8, True, 0.2, 28) == 1
+
+
+def test_packed_buffers_follow_parameter_replacement():
+    """layer.packed() (the buffers the kernels read) re-binds when a per-head
+    parameter is replaced (setattr, load_state_dict(assign=True)) or the module
+    is copied, without walking the 6H parameters on every forward."""
+    import copy
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    torch.manual_seed(0)
+    layer = GraphAttentionLayer(12, 8, num_heads=4, concat=True)
+    pp = layer.packed()
+    assert layer.packed() is pp  # unchanged -> cached
+    # in-place updates (optimizer steps, load_state_dict copies) need no re-bind
+    with torch.no_grad():
+        layer.ws[2].bias.add_(1.0)
+    assert layer.packed() is pp and torch.equal(pp.b[16:24], layer.ws[2].bias)
+    layer.ws[3].weight = torch.nn.Parameter(torch.ones(8, 12))
+    pp2 = layer.packed()
+    assert pp2 is not pp and torch.equal(pp2.w[24:32], torch.ones(8, 12))
+    assert pp2.w[24:32].data_ptr() == layer.ws[3].weight.data_ptr()  # a view again
+    sd = {k: v + 1 for k, v in layer.state_dict().items()}
+    layer.load_state_dict(sd, assign=True)
+    pp3 = layer.packed()
+    for h in range(4):
+        assert torch.equal(pp3.w[8 * h:8 * (h + 1)], sd[f"ws.{h}.weight"])
+        assert torch.equal(pp3.a_dst[8 * h:8 * (h + 1)], sd[f"attentions2.{h}.weight"].view(-1))
+    c = copy.deepcopy(layer)
+    ppc = c.packed()
+    assert ppc.w.data_ptr() == c.ws[0].weight.data_ptr()
+    assert torch.equal(ppc.w, pp3.w) and ppc.w.data_ptr() != pp3.w.data_ptr()

@@ -69,7 +69,7 @@ def main():
                 rc = lib.gat_project_sliced(x.data_ptr(), n, fin, pp.w.data_ptr(),
                                             pp.b.data_ptr(), pp.a_src.data_ptr(),
                                             pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                                            pp.c_dst.data_ptr(), H, F, s, wh.data_ptr(),
+                                            pp.c_dst.data_ptr(), H, F, s, wh.data_ptr(), n,
                                             ss.data_ptr(), H, sd.data_ptr(), stream)
             _lib.check(rc, "project")
         return wh, sd, proj
