@@ -35,12 +35,14 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "../../include/gat_amd.h"
 
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWave = 64;
 
@@ -658,6 +660,162 @@ __global__ __launch_bounds__(256) void k_project_pipe(
                 }
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Projection, software-pipelined K loop, vector-width variant (Fin > 64).
+// Same block shape and MFMA schedule as k_project_pipe (128 rows x BN
+// columns, two 16-row groups per wave, 64-wide K chunks staged through LDS,
+// chunk c+1's loads in flight during chunk c's MFMAs), with the per-element
+// overhead cut:
+//   * x and W chunks load LW floats per lane (LW = 4 when fin % 4 == 0, 2 when
+//     fin % 2 == 0) and land in LDS with one ds_write per load — 4x fewer
+//     address computations, loads and LDS writes than one float per lane;
+//     W rows padded to 68 floats (conflict-free B-fragment reads);
+//   * the attention Linears (GAT.py:44-45) reduce over the head's F lanes by
+//     DPP (no LDS permutes), and lane i of the head's group stores row i;
+//   * Wh goes back through an LDS output tile: each thread stores one fixed
+//     float4 column of 8 rows (coalesced rows, row-major or sliced planes).
+// ---------------------------------------------------------------------------
+template <int NT, int LW>
+__global__ __launch_bounds__(256) void k_project_pipe2(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
+    float* __restrict__ s_dst, int slice_w, long long slice_stride) {
+    constexpr int BK = 64, KS = BK / 4, BN = NT * 16, BM = 128;
+    constexpr int XS = BK + 4, WS = BK + 4, OS = BN + 4;
+    constexpr int XL = BM * BK / (256 * LW);  // x loads per thread per chunk
+    constexpr int WL = BN * BK / (256 * LW);  // W loads per thread per chunk
+    static_assert(OS <= XS, "the output tile reuses the x tile");
+    using vec = typename std::conditional<LW == 4, f32x4,
+                typename std::conditional<LW == 2, f32x2, float>::type>::type;
+    __shared__ __attribute__((aligned(16))) float wsm[BN * WS];
+    __shared__ __attribute__((aligned(16))) float xsm[BM * XS];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int blk0 = blockIdx.x * BM;
+    const int row0 = blk0 + w * 32;
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    vec xn[XL], wn[WL];
+    auto load_chunk = [&](int k0) {
+        // element e = (tid + 256 q) * LW -> row e / 64, k e % 64: consecutive
+        // lanes read consecutive LW-float groups of one row (coalesced).  An LW
+        // group is wholly below or wholly at/after fin (LW divides fin); groups
+        // past fin and rows past n load clamped, in-bounds addresses (their
+        // products meet zeroed W at the LDS write, or feed unstored rows).
+#pragma unroll
+        for (int q = 0; q < XL; ++q) {
+            const int e = (tid + 256 * q) * LW;
+            const int r = min(blk0 + e / BK, n - 1);
+            const int k = min(k0 + e % BK, fin - LW);
+            xn[q] = *reinterpret_cast<const vec*>(X + (size_t)r * fin + k);
+        }
+#pragma unroll
+        for (int q = 0; q < WL; ++q) {
+            const int e = (tid + 256 * q) * LW;
+            const int nn = min(e / BK, HF - 1);
+            const int k = min(k0 + e % BK, fin - LW);
+            wn[q] = *reinterpret_cast<const vec*>(W + (size_t)nn * fin + k);
+        }
+    };
+    load_chunk(0);
+    for (int k0 = 0; k0 < fin; k0 += BK) {
+        __syncthreads();  // the previous chunk's fragment reads are done
+#pragma unroll
+        for (int q = 0; q < XL; ++q) {
+            const int e = (tid + 256 * q) * LW;
+            *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) = xn[q];
+        }
+#pragma unroll
+        for (int q = 0; q < WL; ++q) {
+            const int e = (tid + 256 * q) * LW;
+            const bool ok = e / BK < HF && k0 + e % BK < fin;
+            *reinterpret_cast<vec*>(wsm + (e / BK) * WS + e % BK) = ok ? wn[q] : vec{};
+        }
+        __syncthreads();
+        if (k0 + BK < fin) load_chunk(k0 + BK);  // in flight during this chunk's MFMAs
+        const int ksteps = min(KS, (fin - k0 + 3) / 4);
+        const float* xa0 = xsm + (w * 32 + cl) * XS + kq;
+        const float* xa1 = xa0 + 16 * XS;
+#pragma unroll
+        for (int st = 0; st < KS; ++st) {
+            if (st < ksteps) {  // block-uniform
+                const float a0 = xa0[4 * st], a1v = xa1[4 * st];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const float b = wsm[(t * 16 + cl) * WS + 4 * st + kq];
+                    acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][t], 0, 0, 0);
+                    acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v, b, acc[1][t], 0, 0, 0);
+                }
+            }
+        }
+    }
+    __syncthreads();  // x/W tiles dead: the x tile becomes the output tile
+
+    const int hfp = round_up4(HF);
+    const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
+    float* Os = xsm;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int cc = t * 16 + cl;
+        const float bb = cc < HF ? bW[cc] : 0.f;
+        const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
+        const int h = cc >> lf, li = cl & (F - 1);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            float p1[4], p2[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = acc[g][t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
+                Os[(w * 32 + 16 * g + kq * 4 + i) * OS + cc] = cc < HF ? v : 0.f;
+                p1[i] = group_sum16(v * w1, F);
+                p2[i] = group_sum16(v * w2, F);
+            }
+            // lane li (< 4) of the head's F lanes stores row kq*4 + li's sums
+            if (li < 4 && li < F && h < H) {
+                const float v1 = li == 0 ? p1[0] : li == 1 ? p1[1] : li == 2 ? p1[2] : p1[3];
+                const float v2 = li == 0 ? p2[0] : li == 1 ? p2[1] : li == 2 ? p2[2] : p2[3];
+                const int rr = row0 + 16 * g + kq * 4 + li;
+                if (rr < n) {
+                    if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = v1 + c1[h];
+                    s_dst[(size_t)rr * H + h] = v2 + c2[h];
+                }
+            }
+            if (F < 4 && li == 0 && h < H) {  // heads narrower than 4 lanes: rows F..3
+#pragma unroll
+                for (int i = 1; i < 4; ++i) {
+                    const int rr = row0 + 16 * g + kq * 4 + i;
+                    if (i >= F && rr < n) {
+                        if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
+                        s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // Wh stores: thread owns float4 column c4 (plane offset computed once) of
+    // rows tid / C4 + (256 / C4) * j
+    constexpr int C4 = NT * 4;
+    static_assert(256 % C4 == 0, "NT must divide 16");
+    const int col = 4 * (tid % C4);
+    if (col < hfp) {
+        const int g = col / slice_w;
+        float* dst = Wh + (size_t)g * (size_t)slice_stride + (col - g * slice_w);
+        const int rows = min(BM, n - blk0);
+        for (int r = tid / C4; r < rows; r += 256 / C4)
+            *reinterpret_cast<f32x4*>(dst + (size_t)(blk0 + r) * ld_wh) =
+                *reinterpret_cast<const f32x4*>(Os + r * OS + col);
     }
 }
 
@@ -2341,6 +2499,28 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
                          (long long)n * fin < (1LL << 31) && (pk == nullptr || force_pipe);
     if (pipe_ok) {
         const dim3 gp((n + 127) / 128), bp(256);
+        // vector-width variant (k_project_pipe2; GAT_PROJ_PIPE=1 keeps the
+        // one-float-per-lane kernel): LW floats per lane where fin allows
+        const char* pv = std::getenv("GAT_PROJ_PIPE");
+        const bool pipe2 = (nt == 1 || nt == 2 || nt == 4) && !(pv && std::atoi(pv) == 1);
+        if (pipe2) {
+            const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
+            const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
+#define GAT_PIPE2(NT, LWV)                                                                     \
+    hipLaunchKernelGGL((k_project_pipe2<NT, LWV>), gp, bp, 0, st, x, n, fin, w, b, a_src,     \
+                       c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,      \
+                       slice_w, slice_stride)
+#define GAT_PIPE2_LW(NT)                                  \
+    if (lw == 4) { GAT_PIPE2(NT, 4); }                    \
+    else if (lw == 2) { GAT_PIPE2(NT, 2); }               \
+    else { GAT_PIPE2(NT, 1); }
+            if (nt == 1) { GAT_PIPE2_LW(1) }
+            else if (nt == 2) { GAT_PIPE2_LW(2) }
+            else { GAT_PIPE2_LW(4) }
+#undef GAT_PIPE2_LW
+#undef GAT_PIPE2
+            return status_of(hipGetLastError());
+        }
 #define GAT_PIPE_CASE(NT)                                                                     \
     case NT:                                                                                  \
         hipLaunchKernelGGL((k_project_pipe<NT>), gp, bp, 0, st, x, n, fin, w, b, a_src, c_src, \

@@ -34,6 +34,7 @@ VARIANTS = {
     "proj_direct": {"GAT_PROJ_KERNEL": "direct"},
     "proj_persist": {"GAT_PROJ_KERNEL": "persist"},
     "proj_pipe": {"GAT_PROJ_KERNEL": "pipe"},
+    "proj_pipe1": {"GAT_PROJ_KERNEL": "pipe", "GAT_PROJ_PIPE": "1"},
     "v2": {"GAT_EDGE_V": "2"},
     "v4_natural": {"GAT_EDGE_V": "4", "GAT_EDGE_ORDER": "natural"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
@@ -53,7 +54,8 @@ VARIANTS = {
 @pytest.fixture(params=list(VARIANTS))
 def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
-              "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE"):
+              "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
+              "GAT_PROJ_PIPE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)

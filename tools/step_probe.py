@@ -58,10 +58,14 @@ def main():
     variants = parse_variants(args.variants)
     # PRED (probe-only key): work inserted before each step's projection —
     # fill (an 11.5-MB store kernel), read (an 11.5-MB reduction), sleep (a
-    # ~20 us busy-wait kernel, no memory traffic)
+    # ~20 us busy-wait kernel, no memory traffic), tinyproj (the projection
+    # kernel itself on 64 rows)
     preds = {name: env.pop("PRED", "") for name, env in variants.items()}
     knobs = sorted({k for env in variants.values() for k in env})
     scratch = torch.empty(n, H * F, device=dev)
+    x64 = x[:64].clone()
+    s_dst64 = torch.empty(64, H, device=dev)
+    table64 = None
     res = {name: {"project": [], "project2": [], "edge": [], "step": []} for name in variants}
     stream = torch.cuda.current_stream()
     with torch.no_grad():
@@ -72,6 +76,7 @@ def main():
                 os.environ.update(env)
                 slices = wh_slices(H, F, w.concat, layer.negative_slope, csr.num_edges // n)
                 table = alloc_table(n, H, F, dev, slices=slices)
+                table64 = alloc_table(64, H, F, dev, slices=slices)
                 s_dst = torch.empty(n, H, device=dev)
                 out = torch.empty(n, H * F if w.concat else F, device=dev)
                 evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -87,6 +92,8 @@ def main():
                         scratch.sum()
                     elif preds[name] == "sleep":
                         torch.cuda._sleep(50_000)
+                    elif preds[name] == "tinyproj":  # the same projection kernel, 64 rows
+                        project(x64, pp, H, F, table=table64, s_dst=s_dst64)
                     e[0].record(stream)
                     project(x, pp, H, F, table=table, s_dst=s_dst)
                     e[3].record(stream)
