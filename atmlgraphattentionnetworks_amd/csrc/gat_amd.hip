@@ -1328,16 +1328,20 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
     for (int q = 0; q < V; ++q) a4[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (FUSED) {
+        // a1 pre-scaled by log2(e): the recomputed score comes out in log2 units
         if (c_ok) {
 #pragma unroll
-            for (int q = 0; q < V; ++q) a4[q] = *reinterpret_cast<const f32x4*>(a_src + coff + 4 * q);
+            for (int q = 0; q < V; ++q)
+                a4[q] = *reinterpret_cast<const f32x4*>(a_src + coff + 4 * q) * kLog2e;
         }
         c1 = c_src[h];
     }
     const int e0 = rowptr[r], e1 = rowptr[r + 1];
     const bool kahan = e1 - e0 >= 1024;
     const bool dropping = drop.thresh != 0u;  // kernel-uniform: a scalar branch
-    const float sd = s_dst[(size_t)r * H + h];
+    // the target's share of every score, in log2 units (LeakyReLU is positively
+    // homogeneous: LReLU(z) log2e = LReLU(z log2e)); + c1 when s_src is recomputed
+    const float sd = (s_dst[(size_t)r * H + h] + c1) * kLog2e;
     float m = -INFINITY, l = 0.f;  // running max in log2 units
     // rows of >= 1024 edges keep Kahan-compensated running sums (lc, cmp) over
     // per-chunk partial sums: a 10k-edge hub row otherwise accumulates more fp32
@@ -1371,12 +1375,15 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         if constexpr (FUSED) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                float d = 0.f;
+                // two-lane packed partial sums (v_pk_fma_f32 on the row's own
+                // register pairs, no operand shuffling)
+                f32x2 d2 = f32x2{0.f, 0.f};
 #pragma unroll
-                for (int q = 0; q < V; ++q)
-                    d = fmaf(v[u][q].w, a4[q].w, fmaf(v[u][q].z, a4[q].z,
-                        fmaf(v[u][q].y, a4[q].y, fmaf(v[u][q].x, a4[q].x, d))));
-                s[u] = d;
+                for (int q = 0; q < V; ++q) {
+                    d2 += f32x2{v[u][q].x, v[u][q].y} * f32x2{a4[q].x, a4[q].y};
+                    d2 += f32x2{v[u][q].z, v[u][q].w} * f32x2{a4[q].z, a4[q].w};
+                }
+                s[u] = d2.x + d2.y;
             }
             const int hl = F / (4 * V);  // lanes per head
             if (hl > 1) {
@@ -1389,14 +1396,15 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                         for (int u = 0; u < U; ++u) s[u] += __shfl_xor(s[u], off);
                 }
             }
+        } else {
 #pragma unroll
-            for (int u = 0; u < U; ++u) s[u] += c1;
+            for (int u = 0; u < U; ++u) s[u] *= kLog2e;  // gathered s_src: natural units
         }
         float emax = -INFINITY;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const float z = sd + s[u];
-            s[u] = u < nk ? fmaxf(z, z * slope) * kLog2e : -INFINITY;  // slope in [0, 1]
+            const float z = sd + s[u];  // log2 units
+            s[u] = u < nk ? fmaxf(z, z * slope) : -INFINITY;  // slope in [0, 1]
             emax = fmaxf(emax, s[u]);
         }
         const float m_new = fmaxf(m, emax);
