@@ -353,6 +353,12 @@ __device__ __forceinline__ float dpp_mov(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
+// lane k of each quad, to all four lanes of the quad (DPP quad_perm [k,k,k,k])
+template <int K>
+__device__ __forceinline__ int quad_bcast(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, K * 0x55, 0xF, 0xF, false);
+}
+
 __device__ __forceinline__ float group_sum16(float v, int w) {
     if (w >= 2) v += dpp_mov<0xB1>(v);
     if (w >= 4) v += dpp_mov<0x4E>(v);
@@ -1305,10 +1311,16 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     float* __restrict__ lse, DropArgs drop_arg, float* __restrict__ y_heads,
     int nslices, int slice_w, long long slice_stride) {
     const DropArgs drop = resolve_drop(drop_arg);
-    constexpr int CL = (U + G - 1) / G;  // col values held per lane per chunk
+    // col values held per lane per chunk.  Groups of >= 4 lanes: every quad of
+    // the group holds the chunk's indices (lane c: edges (c & 3) + 4t), so the
+    // source ids are broadcast by DPP within the quad instead of LDS permutes
+    constexpr bool QB = G >= 4 && U % 4 == 0;
+    constexpr int CL = QB ? U / 4 : (U + G - 1) / G;
     const int lane = threadIdx.x & 63;
     const int c = lane & (G - 1);
     const int gbase = lane & ~(G - 1);
+    const int cstep = QB ? 4 : G;        // col slot stride per held value
+    const int cfirst = QB ? (c & 3) : c;  // this lane's first col slot
     // sliced node table (nslices > 1): block b works on column slice b % nslices,
     // so with round-robin block placement one XCD gathers from one slice plane
     // only — an [N, slice_w] plane small enough to stay in that XCD's L2
@@ -1355,12 +1367,22 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     // chunk k gathers (loads unconditional, clamped to the row's last edge)
     int cv[CL];
 #pragma unroll
-    for (int t = 0; t < CL; ++t) cv[t] = col[min(e0 + c + t * G, e1 - 1)];
+    for (int t = 0; t < CL; ++t) cv[t] = col[min(e0 + cfirst + t * cstep, e1 - 1)];
     // gathers of one chunk: source ids broadcast from the group's col values
     auto fetch = [&](const int (&cc)[CL], f32x4 (&v)[U][V], float (&s)[U]) {
         int j[U];
+        if constexpr (QB) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) j[u] = __shfl(cc[u / G], gbase + (u % G));
+            for (int u = 0; u < U; u += 4) {
+                j[u + 0] = quad_bcast<0>(cc[u / 4]);
+                j[u + 1] = quad_bcast<1>(cc[u / 4]);
+                j[u + 2] = quad_bcast<2>(cc[u / 4]);
+                j[u + 3] = quad_bcast<3>(cc[u / 4]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) j[u] = __shfl(cc[u / G], gbase + (u % G));
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float* row = Whs + (size_t)j[u] * ld_wh;
@@ -1462,11 +1484,11 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         fetch(cv, vc, sc);
         int cn[CL];
 #pragma unroll
-        for (int t = 0; t < CL; ++t) cn[t] = col[min(e0 + U + c + t * G, e1 - 1)];
+        for (int t = 0; t < CL; ++t) cn[t] = col[min(e0 + U + cfirst + t * cstep, e1 - 1)];
         for (int k = e0; k < e1; k += U) {
             int cnn[CL];
 #pragma unroll
-            for (int t = 0; t < CL; ++t) cnn[t] = col[min(k + 2 * U + c + t * G, e1 - 1)];
+            for (int t = 0; t < CL; ++t) cnn[t] = col[min(k + 2 * U + cfirst + t * cstep, e1 - 1)];
             f32x4 vn[U][V];
             float sn[U];
             if (k + U < e1) fetch(cn, vn, sn);
@@ -1484,7 +1506,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         for (int k = e0; k < e1; k += U) {
             int cn[CL];
 #pragma unroll
-            for (int t = 0; t < CL; ++t) cn[t] = col[min(k + U + c + t * G, e1 - 1)];
+            for (int t = 0; t < CL; ++t) cn[t] = col[min(k + U + cfirst + t * cstep, e1 - 1)];
             f32x4 v[U][V];
             float s[U];
             fetch(cv, v, s);
