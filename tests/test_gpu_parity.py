@@ -289,3 +289,30 @@ def test_sliced_entry_points_reject_unsupported_shapes():
     # fin > 64 needs the pipelined projection: f a power of two <= 16, hf <= 64
     assert lib.gat_project_sliced(p, 1, 100, p, p, p, p, p, p, 8, 12, 2, p, 1, p, 8, p,
                                   st) == _lib.GAT_EUNSUPPORTED
+
+
+def test_sliced_default_with_unaligned_x_view():
+    """x as a row view that starts off a 16-B boundary (fin = 50): the whole-K
+    projection that writes the sliced table needs 16-B aligned rows, so the
+    layer falls back to the row-major path; results still match the oracle."""
+    from atmlgraphattentionnetworks_amd import _lib
+    n, e, fin, H, F = 1500, 30000, 50, 8, 8
+    x, ei, state = random_case(n + 1, e, fin, H, F, True, seed=11)
+    layer = layer_from_state(state, fin, F, H, True)
+    xd = x.to(dev())[1:]                 # 200-B offset
+    assert xd.data_ptr() % 16 != 0
+    ei = ei[:, (ei[0] >= 1) & (ei[1] >= 1)] - 1
+    with torch.no_grad():
+        out = layer(xd, ei.to(dev())).cpu()
+    ref = gat_layer_forward_from_state(state, x[1:], ei, H, True)
+    torch.testing.assert_close(out, ref, atol=ATOL, rtol=RTOL)
+    # the sliced projection itself refuses the unaligned rows (nothing launched)
+    pp = layer.packed()
+    wh = torch.empty(2 * n * 32, device=dev())
+    sd = torch.empty(n * H, device=dev())
+    lib = _lib.load()
+    rc = lib.gat_project_sliced(xd.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                                pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
+                                pp.c_dst.data_ptr(), H, F, 2, wh.data_ptr(), n, None, H,
+                                sd.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert rc == _lib.GAT_EUNSUPPORTED
