@@ -17,7 +17,9 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 3
+GAT_ABI_VERSION = 4
+GAT_SEG_LOAD = 1
+GAT_SEG_STORE = 2
 GAT_MAX_HEADS = 64
 GAT_MAX_HF = 256
 GAT_ACT_LEAKY_RELU = 0
@@ -33,6 +35,7 @@ _c_u64 = ctypes.c_ulonglong
 # symbol -> (restype, argtypes); mirrors include/gat_amd.h line for line
 SIGNATURES = {
     "gat_abi_version": (_c_int, []),
+    "gat_tuning_reload": (_c_int, []),
     "gat_table_layout": (_c_int, [_c_int, _c_int, _c_int_p, _c_int_p]),
     "gat_project": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                              _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp]),
@@ -45,6 +48,12 @@ SIGNATURES = {
     "gat_edge_aggregate_sliced": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
                                            _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_float,
                                            _c_vp, _c_vp, _c_int, _c_vp]),
+    "gat_edge_aggregate_seg": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_int,
+                                        _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp,
+                                        _c_int, _c_int, _c_int, _c_float, _c_vp, _c_vp, _c_int,
+                                        _c_int, _c_vp, _c_vp, _c_int, _c_vp]),
+    "gat_edge_merge": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_int,
+                                _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gat_csr_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csr_build": (_c_int, [_c_vp, _c_ll, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, ctypes.c_size_t,
                                _c_vp, _c_vp]),
@@ -86,6 +95,10 @@ _lib = None
 
 class GatLibraryError(RuntimeError):
     """Raised on a non-zero status from the HIP library."""
+
+
+def is_loaded() -> bool:
+    return _lib is not None
 
 
 def load() -> ctypes.CDLL:

@@ -21,8 +21,10 @@
 //       ld_s = ld_wh (gat_table_layout).
 //   s_dst[n_nodes][H] fp32 (target term, read once per row)
 //   CSR by target: rowptr int32 [n+1], col int32 [E+n]; within a row the
-//   input edge order is kept (stable sort) and the self-loop is last,
-//   exactly the order add_self_loops produces.
+//   sources ascend (one stable radix sort of (target, source) keys over the
+//   input edges plus the appended self-loops; duplicates keep input order).
+//   The segmented softmax and the sum are order-independent up to fp32
+//   rounding, which the 1e-5 parity bar covers.
 //
 // Everything is fp32 (parity bar 1e-5 vs the reference's fp32 CPU path).
 // No CUDA shims, no hipify, no multi-backend code: gfx950 only.
@@ -97,7 +99,8 @@ __host__ __device__ constexpr int round_up4(int v) { return (v + 3) & ~3; }
 // of (seed, k, h) — a counter-based hash — so the backward pass regenerates the
 // forward's mask without storing it.  keep <=> mix(seed, k*H + h) >= thresh,
 // thresh = round(p * 2^32); kept coefficients are scaled by 1/(1-p).
-// tests/test_dropout_hash.py restates the hash in numpy.
+// oracle.dropout_factors restates the hash in numpy (tests/test_gpu_training.py
+// checks forward and gradients against it).
 struct DropArgs {
     unsigned thresh;   // 0: no dropout
     float scale;       // 1 / (1 - p)
@@ -368,313 +371,17 @@ __device__ __forceinline__ float group_sum16(float v, int w) {
 }
 
 // ---------------------------------------------------------------------------
-// Projection, persistent and pipelined over row tiles (Fin <= 64, H*F <= 64);
-// an A/B alternative to k_project_wk (GAT_PROJ_KERNEL=persist), measured
-// slower at PPI shape.  The idea: k_project_wk launches one 64-row tile per
-// block and all of them fit on the chip at once, so every block loads, computes
-// and stores in lockstep.  Here a fixed grid of blocks loops over tiles
-// t = blockIdx, blockIdx + grid, ...: W and the epilogue parameters go to LDS
-// once per block, x tiles are double-buffered in LDS, and tile t + grid's x
-// is in flight (4 float4 per thread) while tile t is computed and stored.
-// LDS (floats): W [BN x fin] | x [2][64 x fin] | out [64 x (BN+4)] | params.
-// ---------------------------------------------------------------------------
-__host__ __device__ inline int persist_lds_floats(int fin, int nt) {
-    const int bn = nt * 16;
-    const int w = (bn * fin + 3) & ~3, x = (64 * fin + 3) & ~3, o = 64 * (bn + 4);
-    return w + 2 * x + o + 3 * bn + 128;
-}
-
-template <int NT>
-__global__ __launch_bounds__(256) void k_project_persist(
-    const float* __restrict__ X, int n, int fin,
-    const float* __restrict__ W, const float* __restrict__ bW,
-    const float* __restrict__ a1, const float* __restrict__ c1,
-    const float* __restrict__ a2, const float* __restrict__ c2,
-    int H, int F, int HF, float* __restrict__ Wh, int ld_wh,
-    float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst) {
-    constexpr int BM = 64, BN = NT * 16, OS = BN + 4, XQ = BM * 64 / 1024;  // float4 / thread
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int cl = lane & 15, kq = lane >> 4;
-    const int wn = (BN * fin + 3) & ~3, xn = (BM * fin + 3) & ~3;
-    float* Ws = smem;
-    float* Xs0 = smem + wn;
-    float* Os = Xs0 + 2 * xn;
-    float* bs = Os + BM * OS;
-    float* a1s = bs + BN;
-    float* a2s = bs + 2 * BN;
-    float* c1s = bs + 3 * BN;
-    float* c2s = c1s + 64;
-    const int ntiles = (n + BM - 1) / BM;
-    const long long total = (long long)n * fin;
-    const long long last4 = (total & ~3LL) - 4;  // start of the array's last full float4
-
-    // x tile -> registers: unconditional float4 loads at addresses clamped into
-    // the array (rows past n are never stored); the <= 3 floats after the last
-    // full float4 come as scalars
-    f32x4 xv[XQ];
-    float xt[3];
-    auto load_x = [&](int t) {
-        const long long base = (long long)t * BM * fin;
-#pragma unroll
-        for (int q = 0; q < XQ; ++q) {
-            const long long i = base + 4LL * (tid + 256 * q);
-            xv[q] = *reinterpret_cast<const f32x4*>(X + (i < last4 ? i : last4));
-        }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const long long i = (total & ~3LL) + j;
-            xt[j] = X[i < total ? i : total - 1];
-        }
-    };
-    auto store_x = [&](int t, float* Xs) {
-        const long long base = (long long)t * BM * fin;
-        const int cnt = (int)min((long long)BM * fin, total - base);
-        const int cnt4 = (int)(min(base + cnt, total & ~3LL) - base);  // full float4s
-#pragma unroll
-        for (int q = 0; q < XQ; ++q) {
-            const int i = 4 * (tid + 256 * q);
-            if (i < cnt4) *reinterpret_cast<f32x4*>(Xs + i) = xv[q];
-        }
-        if (tid == 0)
-            for (int j = 0; cnt4 + j < cnt && j < 3; ++j) Xs[cnt4 + j] = xt[j];
-    };
-
-    // once per block: W (rows >= HF zero) and the epilogue parameters
-    for (int i = tid; i < BN * fin; i += 256) Ws[i] = i < HF * fin ? W[i] : 0.f;
-    if (tid < BN) {
-        const bool ok = tid < HF;
-        const int cc = ok ? tid : 0;
-        const float bv = bW[cc], av1 = a1[cc], av2 = a2[cc];
-        bs[tid] = ok ? bv : 0.f;
-        a1s[tid] = ok ? av1 : 0.f;
-        a2s[tid] = ok ? av2 : 0.f;
-    }
-    if (tid < H) {
-        const float v1 = c1[tid], v2 = c2[tid];
-        c1s[tid] = v1;
-        c2s[tid] = v2;
-    }
-    int t = blockIdx.x;
-    if (t < ntiles) {
-        load_x(t);
-        store_x(t, Xs0);
-    }
-    __syncthreads();
-    const int hfp = round_up4(HF), c4n = hfp / 4;
-    for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
-        float* Xs = Xs0 + (it & 1) * xn;
-        const int tn = t + gridDim.x;
-        if (tn < ntiles) load_x(tn);  // in flight during this tile's MFMAs and stores
-
-        f32x4 acc[NT];
-#pragma unroll
-        for (int q = 0; q < NT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* xa = Xs + (w * 16 + cl) * fin + kq;
-        const float* wb = Ws + cl * fin + kq;
-        const int ks = fin / 4;
-        for (int s4 = 0; s4 < ks; ++s4) {
-            const float a = xa[4 * s4];
-#pragma unroll
-            for (int q = 0; q < NT; ++q)
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[q * 16 * fin + 4 * s4], acc[q],
-                                                              0, 0, 0);
-        }
-        if (fin & 3) {  // last partial k-step
-            const bool ok = 4 * ks + kq < fin;
-            const float a = ok ? xa[4 * ks] : 0.f;
-#pragma unroll
-            for (int q = 0; q < NT; ++q) {
-                const float b = ok ? wb[q * 16 * fin + 4 * ks] : 0.f;
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[q], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < NT; ++q) {
-            const int cc = q * 16 + cl;
-            const float bb = bs[cc];  // Linear bias inside Wh (GAT.py:43); 0 past HF
-#pragma unroll
-            for (int i = 0; i < 4; ++i) Os[(w * 16 + kq * 4 + i) * OS + cc] = acc[q][i] + bb;
-        }
-        __syncthreads();
-        const int row0 = t * BM, rows = min(BM, n - row0);
-        for (int idx = tid; idx < rows * c4n; idx += 256) {
-            const int r = idx / c4n, c4 = idx - r * c4n;
-            f32x4 v = *reinterpret_cast<const f32x4*>(Os + r * OS + 4 * c4);
-            if (4 * c4 + 3 >= HF) {  // zero the pad columns [HF, hfp)
-                if (4 * c4 + 0 >= HF) v.x = 0.f;
-                if (4 * c4 + 1 >= HF) v.y = 0.f;
-                if (4 * c4 + 2 >= HF) v.z = 0.f;
-                if (4 * c4 + 3 >= HF) v.w = 0.f;
-            }
-            *reinterpret_cast<f32x4*>(Wh + (size_t)(row0 + r) * ld_wh + 4 * c4) = v;
-        }
-        // attention Linears on the fp32 Wh (GAT.py:44-45): s = Wh_h . a_h + c_h
-        for (int idx = tid; idx < rows * H; idx += 256) {
-            const int r = idx / H, h = idx - r * H;
-            const float* o = Os + r * OS + h * F;
-            const float* p1 = a1s + h * F;
-            const float* p2 = a2s + h * F;
-            float v1 = 0.f, v2 = 0.f;
-            for (int f = 0; f < F; ++f) {
-                v1 = fmaf(o[f], p1[f], v1);
-                v2 = fmaf(o[f], p2[f], v2);
-            }
-            Ss[(size_t)(row0 + r) * ld_s + h] = v1 + c1s[h];
-            s_dst[(size_t)(row0 + r) * H + h] = v2 + c2s[h];
-        }
-        if (tn < ntiles) store_x(tn, Xs0 + ((it + 1) & 1) * xn);
-        __syncthreads();  // next tile's x in LDS; this tile's out reads done
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Projection, software-pipelined K loop (Fin > 64).  fp32 MFMA throughput
 // (157 TF) bounds a [N, Fin] x [Fin, 64] projection at large Fin (Reddit:
-// 18 GFLOP -> 115 us).  The K-tiled kernel reads its MFMA A operand straight
-// from global memory, 16 rows x 16 B per load instruction, so every x cache
-// line passes through L1 eight times.  Here:
+// 18 GFLOP -> 115 us).
 //   * block = 128 rows x BN (<= 64) columns; wave w owns rows [32w, 32w+32)
 //     as two 16-row groups, so every W fragment read from LDS feeds two MFMAs;
 //   * per 64-wide K chunk, x [128 x 64] and W [BN x 64] are staged through
-//     LDS with fully coalesced loads (64 lanes = one 256-B row chunk) and the
-//     A/B fragments read back conflict-free (row strides 68 and 66);
-//   * chunk c+1's x and W loads are in flight in registers while chunk c's
-//     16 k-steps x 8 MFMAs run; two barriers per chunk.
-// Epilogue: bias, Wh store, score dot products by shuffles within F lanes.
-// ---------------------------------------------------------------------------
-template <int NT>
-__global__ __launch_bounds__(256) void k_project_pipe(
-    const float* __restrict__ X, int n, int fin,
-    const float* __restrict__ W, const float* __restrict__ bW,
-    const float* __restrict__ a1, const float* __restrict__ c1,
-    const float* __restrict__ a2, const float* __restrict__ c2,
-    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
-    float* __restrict__ s_dst, int slice_w, long long slice_stride) {
-    constexpr int BK = 64, KS = BK / 4, BN = NT * 16, BM = 128;
-    constexpr int WL = BN * BK / 256;  // W-tile elements per thread
-    constexpr int XL = BM * BK / 256;  // x-tile elements per thread (32)
-    constexpr int WS = BK + 2, XS = BK + 4;
-    __shared__ float wsm[BN * WS];
-    __shared__ float xsm[BM * XS];
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int cl = lane & 15, kq = lane >> 4;
-    const int blk0 = blockIdx.x * BM;
-    const int row0 = blk0 + w * 32;
-    f32x4 acc[2][NT];
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    float xn[XL], wn[WL];
-    auto load_chunk = [&](int k0) {
-        // x: element idx = tid + 256 q -> row idx / 64, k idx % 64: one wave
-        // instruction reads one row's 64 consecutive k (coalesced)
-        // Raw loads only (no math on the loaded values until the LDS write, so
-        // nothing forces a wait between them).  Clamped addresses keep every
-        // load in bounds: x rows >= n feed output rows that are never stored,
-        // and k >= fin is zeroed on the W side at the LDS write, so x needs no
-        // mask.  32-bit element offsets (n * fin < 2^31, checked at launch).
-        const unsigned kc = (unsigned)min(k0 + (tid & 63), fin - 1);
-#pragma unroll
-        for (int q = 0; q < XL; ++q) {
-            const int r = min(blk0 + (tid >> 6) + 4 * q, n - 1);
-            xn[q] = X[(unsigned)r * (unsigned)fin + kc];
-        }
-#pragma unroll
-        for (int q = 0; q < WL; ++q) {
-            const int idx = tid + q * 256;
-            const int nn = min(idx / BK, HF - 1), gk = min(k0 + idx % BK, fin - 1);
-            wn[q] = W[(unsigned)nn * (unsigned)fin + (unsigned)gk];
-        }
-    };
-    load_chunk(0);
-    for (int k0 = 0; k0 < fin; k0 += BK) {
-        __syncthreads();  // the previous chunk's fragment reads are done
-#pragma unroll
-        for (int q = 0; q < XL; ++q) xsm[((tid >> 6) + 4 * q) * XS + (tid & 63)] = xn[q];
-#pragma unroll
-        for (int q = 0; q < WL; ++q) {
-            const int idx = tid + q * 256;
-            const bool ok = idx / BK < HF && k0 + idx % BK < fin;
-            wsm[(idx / BK) * WS + idx % BK] = ok ? wn[q] : 0.f;
-        }
-        __syncthreads();
-        if (k0 + BK < fin) load_chunk(k0 + BK);  // in flight during this chunk's MFMAs
-        const int ksteps = min(KS, (fin - k0 + 3) / 4);
-        const float* xa0 = xsm + (w * 32 + cl) * XS + kq;
-        const float* xa1 = xa0 + 16 * XS;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            if (s < ksteps) {  // block-uniform
-                const float a0 = xa0[4 * s], a1v = xa1[4 * s];
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    const float b = wsm[(t * 16 + cl) * WS + 4 * s + kq];
-                    acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][t], 0, 0, 0);
-                    acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v, b, acc[1][t], 0, 0, 0);
-                }
-            }
-        }
-    }
-
-    const int hfp = round_up4(HF);
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-        const int rbase = row0 + 16 * g + (lane >> 4) * 4;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int cc = t * 16 + cl;
-            const float bb = cc < HF ? bW[cc] : 0.f;
-            const int sg = cc / slice_w;  // slice plane of this column (0 unsliced)
-            float* whc = Wh + (size_t)sg * (size_t)slice_stride + (cc - sg * slice_w);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float v = acc[g][t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
-                acc[g][t][i] = v;
-                const int rr = rbase + i;
-                if (rr < n && cc < hfp) whc[(size_t)rr * ld_wh] = v;
-            }
-        }
-        // scores: head = F consecutive lanes of one 16-column tile (F | 16)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int cc = t * 16 + cl;
-            const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
-            float p1[4], p2[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                p1[i] = acc[g][t][i] * w1;
-                p2[i] = acc[g][t][i] * w2;
-            }
-            for (int off = 1; off < F; off <<= 1)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    p1[i] += __shfl_xor(p1[i], off);
-                    p2[i] += __shfl_xor(p2[i], off);
-                }
-            const int h = cc / F;
-            if ((cl & (F - 1)) == 0 && h < H) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int rr = rbase + i;
-                    if (rr >= n) continue;
-                    if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
-                    s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
-                }
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Projection, software-pipelined K loop, vector-width variant (Fin > 64).
-// Same block shape and MFMA schedule as k_project_pipe (128 rows x BN
-// columns, two 16-row groups per wave, 64-wide K chunks staged through LDS,
-// chunk c+1's loads in flight during chunk c's MFMAs), with the per-element
-// overhead cut:
+//     LDS with fully coalesced loads, and chunk c+1's loads are in flight in
+//     registers while chunk c's 16 k-steps x 8 MFMAs run; two barriers per
+//     chunk.
+// Per-element overhead (measured against a one-float-per-lane version of the
+// same schedule):
 //   * x and W chunks load LW floats per lane (LW = 4 when fin % 4 == 0, 2 when
 //     fin % 2 == 0) and land in LDS with one ds_write per load — 4x fewer
 //     address computations, loads and LDS writes than one float per lane;
@@ -822,123 +529,6 @@ __global__ __launch_bounds__(256) void k_project_pipe2(
         for (int r = tid / C4; r < rows; r += 256 / C4)
             *reinterpret_cast<f32x4*>(dst + (size_t)(blk0 + r) * ld_wh) =
                 *reinterpret_cast<const f32x4*>(Os + r * OS + col);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Projection, direct-load variant (F a power of two): one wave owns 16 node
-// rows x TW column tiles (TW*16 columns, whole heads), so a PPI-shape layer
-// runs 2x the waves of the LDS-tiled kernel.  MFMA A/B fragments are loaded
-// straight to registers — X rows once, W (a few KB) from L1/L2 — in K chunks
-// of 16/TW k-steps with the next chunk in flight during the current MFMAs; no
-// LDS, no barriers.  Epilogue parameters are loaded up front; the score dot
-// products are summed across the head's lanes with DPP.
-// ---------------------------------------------------------------------------
-template <int TW>
-__global__ __launch_bounds__(256) void k_project_direct(
-    const float* __restrict__ X, int n, int fin,
-    const float* __restrict__ W, const float* __restrict__ bW,
-    const float* __restrict__ a1, const float* __restrict__ c1,
-    const float* __restrict__ a2, const float* __restrict__ c2,
-    int H, int F, int HF, int col_groups, float* __restrict__ Wh, int ld_wh,
-    float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst) {
-    constexpr int KC = TW >= 16 ? 1 : 16 / TW;  // k-steps (of 4) per chunk: ~KC*(1+TW) loads
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int rg = wave / col_groups, cg = wave % col_groups;
-    const int row0 = rg * 16;
-    if (row0 >= n) return;
-    const int cl = lane & 15, kq = lane >> 4;
-    const int hfp = round_up4(HF);
-    const float* xr = X + (size_t)min(row0 + cl, n - 1) * fin;
-    const float* wr[TW];
-    float wm[TW], bb[TW], w1[TW], w2[TW];
-#pragma unroll
-    for (int t = 0; t < TW; ++t) {
-        const int cc = (cg * TW + t) * 16 + cl;
-        const bool ok = cc < HF;
-        wr[t] = W + (size_t)min(cc, HF - 1) * fin;
-        wm[t] = ok ? 1.f : 0.f;
-        bb[t] = bW[min(cc, HF - 1)] * wm[t];  // epilogue parameters, loaded up front
-        w1[t] = a1[min(cc, HF - 1)] * wm[t];
-        w2[t] = a2[min(cc, HF - 1)] * wm[t];
-    }
-    f32x4 acc[TW];
-#pragma unroll
-    for (int t = 0; t < TW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // loads are unconditional (clamped address x 0/1 mask): a guarded load
-    // compiles to a branch + vmcnt(0) per element
-    float xa[KC], wa[KC][TW];
-    auto load_chunk = [&](int k0, float (&xs)[KC], float (&ws)[KC][TW]) {
-#pragma unroll
-        for (int s = 0; s < KC; ++s) {
-            const int kk = k0 + 4 * s + kq;
-            const float km = kk < fin ? 1.f : 0.f;
-            const int kc = min(kk, fin - 1);
-            xs[s] = xr[kc] * km;
-#pragma unroll
-            for (int t = 0; t < TW; ++t) ws[s][t] = wr[t][kc] * wm[t];
-        }
-    };
-    if (fin > 0) load_chunk(0, xa, wa);
-    for (int k0 = 0; k0 < fin; k0 += 4 * KC) {
-        const bool more = k0 + 4 * KC < fin;
-        float xb[KC], wb[KC][TW];
-        if (more) load_chunk(k0 + 4 * KC, xb, wb);
-        const int steps = min(KC, (fin - k0 + 3) / 4);
-#pragma unroll
-        for (int s = 0; s < KC; ++s) {
-            if (s < steps) {  // wave-uniform
-#pragma unroll
-                for (int t = 0; t < TW; ++t)
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], wa[s][t], acc[t], 0, 0, 0);
-            }
-        }
-        if (more) {
-#pragma unroll
-            for (int s = 0; s < KC; ++s) {
-                xa[s] = xb[s];
-#pragma unroll
-                for (int t = 0; t < TW; ++t) wa[s][t] = wb[s][t];
-            }
-        }
-    }
-
-    // accumulator map: column (cg*TW + t)*16 + cl, rows (lane >> 4) * 4 + i
-    float p1[4] = {0.f, 0.f, 0.f, 0.f}, p2[4] = {0.f, 0.f, 0.f, 0.f};
-    const int tph = F >= 16 ? F / 16 : 1;  // tiles per head
-#pragma unroll
-    for (int t = 0; t < TW; ++t) {
-        const int cc = (cg * TW + t) * 16 + cl;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float v = acc[t][i] + bb[t];  // Linear bias inside Wh (GAT.py:43)
-            const int rr = row0 + (lane >> 4) * 4 + i;
-            if (rr < n && cc < hfp) Wh[(size_t)rr * ld_wh + cc] = v;
-            p1[i] = fmaf(v, w1[t], p1[i]);
-            p2[i] = fmaf(v, w2[t], p2[i]);
-        }
-        if ((t + 1) % tph == 0) {  // p1/p2 now hold this lane's share of a whole head
-            const int gw = F < 16 ? F : 16;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                p1[i] = group_sum16(p1[i], gw);
-                p2[i] = group_sum16(p2[i], gw);
-            }
-            const int h = cc / F;
-            if ((cl & (gw - 1)) == 0 && h < H) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int rr = row0 + (lane >> 4) * 4 + i;
-                    if (rr >= n) continue;
-                    Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
-                    s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) p1[i] = p2[i] = 0.f;
-        }
     }
 }
 
@@ -1296,13 +886,47 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 // row_order (optional): target rows in descending in-degree order, so the
 // rows sharing a wave have near-equal lengths and the heaviest start first.
 // Head mean (concat=False, F/4V a power of two) is an xor-butterfly.
+//
+// Rows are described by an EdgeRows: the edge range of a row is
+// [eb[i], ee[i]) with i = the row id (eb = rowptr, ee = rowptr + 1 for the
+// plain forward) or, by_pos, the schedule position.  A row may be a SEGMENT
+// of a target row's in-edges, with the online-softmax state (m in log2 units,
+// l, un-normalised acc) carried in memory:
+//   * multi-GPU passes (distributed.py): pass c covers the sources that arrived
+//     with all-gather chunk c, loading the state pass c-1 stored;
+//   * hub rows (degree skew): the segments of one long row run in parallel as
+//     separate "virtual rows", and k_edge_merge combines their states.
 // ---------------------------------------------------------------------------
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
+struct EdgeRows {
+    const int* eb;     // segment begin (CSR position), indexed by row id or position
+    const int* ee;     // segment end
+    float* st_acc;     // carried state: un-normalised accumulators [.., ld_st]
+    float* st_ml;      // carried state: per head (m in log2 units, l) as [.., 2H]
+    int ld_st;         // floats per st_acc row
+    int by_pos;        // eb/ee/state indexed by schedule position (else by row id)
+    int load;          // start from the stored state
+    int store_lt;      // positions < store_lt store the state instead of the output
+};
+
+EdgeRows rows_of_csr(const int* rowptr) {
+    EdgeRows e;
+    e.eb = rowptr;
+    e.ee = rowptr + 1;
+    e.st_acc = nullptr;
+    e.st_ml = nullptr;
+    e.ld_st = 0;
+    e.by_pos = 0;
+    e.load = 0;
+    e.store_lt = 0;
+    return e;
+}
+
 template <int G, int U, int V, bool FUSED, bool PIPE = false>
 __global__ __launch_bounds__(256) void k_edge_grp(
-    const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
+    const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
     const float* __restrict__ Wh, int ld_wh, const float* __restrict__ Ss, int ld_s,
     const float* __restrict__ a_src, const float* __restrict__ c_src,
@@ -1348,7 +972,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         }
         c1 = c_src[h];
     }
-    const int e0 = rowptr[r], e1 = rowptr[r + 1];
+    const int si = er.by_pos ? pos : r;  // segment / state index
+    const int e0 = er.eb[si], e1 = er.ee[si];
     const bool kahan = e1 - e0 >= 1024;
     const bool dropping = drop.thresh != 0u;  // kernel-uniform: a scalar branch
     // the target's share of every score, in log2 units (LeakyReLU is positively
@@ -1362,12 +987,23 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     float lc = 0.f;
 #pragma unroll
     for (int q = 0; q < V; ++q) acc[q] = cmp[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (er.load) {  // continue a row whose earlier segments a previous pass ran
+        m = er.st_ml[(size_t)si * 2 * H + h];
+        l = er.st_ml[(size_t)si * 2 * H + H + h];
+        if (c_ok) {
+#pragma unroll
+            for (int q = 0; q < V; ++q)
+                acc[q] = *reinterpret_cast<const f32x4*>(er.st_acc + (size_t)si * er.ld_st + coff + 4 * q);
+        }
+    }
 
     // col indices are software-pipelined: chunk k+U's are in flight while
     // chunk k gathers (loads unconditional, clamped to the row's last edge)
     int cv[CL];
 #pragma unroll
-    for (int t = 0; t < CL; ++t) cv[t] = col[min(e0 + cfirst + t * cstep, e1 - 1)];
+    // an empty row (possible only through a caller-built CSR: gat_csr_build adds a
+    // self-loop to every row) loads nothing and stores the bias
+    for (int t = 0; t < CL; ++t) cv[t] = e1 > e0 ? col[min(e0 + cfirst + t * cstep, e1 - 1)] : 0;
     // gathers of one chunk: source ids broadcast from the group's col values
     auto fetch = [&](const int (&cc)[CL], f32x4 (&v)[U][V], float (&s)[U]) {
         int j[U];
@@ -1484,7 +1120,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         fetch(cv, vc, sc);
         int cn[CL];
 #pragma unroll
-        for (int t = 0; t < CL; ++t) cn[t] = col[min(e0 + U + cfirst + t * cstep, e1 - 1)];
+        for (int t = 0; t < CL; ++t) cn[t] = e1 > e0 ? col[min(e0 + U + cfirst + t * cstep, e1 - 1)] : 0;
         for (int k = e0; k < e1; k += U) {
             int cnn[CL];
 #pragma unroll
@@ -1516,6 +1152,19 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         }
     }
 
+    if (pos < er.store_lt) {  // a segment: hand the state on (the row is not finished)
+        if (c_ok) {
+#pragma unroll
+            for (int q = 0; q < V; ++q)
+                *reinterpret_cast<f32x4*>(er.st_acc + (size_t)si * er.ld_st + coff + 4 * q) =
+                    kahan ? acc[q] - cmp[q] : acc[q];
+            if ((coff % F) == 0) {
+                er.st_ml[(size_t)si * 2 * H + h] = m;
+                er.st_ml[(size_t)si * 2 * H + H + h] = kahan ? l - lc : l;
+            }
+        }
+        return;
+    }
     const float inv = 1.f / (l + 1e-16f);
     if (lse != nullptr && c_ok && (coff % F) == 0)
         lse[(size_t)r * H + h] = (m + log2f(l)) * kLn2;  // natural-log units
@@ -1558,6 +1207,61 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 o[2] = y[q].z / hh + bias[f0 + 2];
                 o[3] = y[q].w / hh + bias[f0 + 3];
             }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Merge of split hub rows (degree skew).  A target row with more in-edges
+// than one lane group should walk serially is cut into segments that run as
+// separate virtual rows of k_edge_grp (EdgeRows by_pos + store), in parallel;
+// hub k's segment states are virtual rows [vptr[k], vptr[k+1]).  Per head:
+//   M = max_s m_s,  L = sum_s l_s 2^(m_s - M),  y = sum_s acc_s 2^(m_s - M) / (L + 1e-16)
+// which is the segmented softmax of PyG utils.softmax (GAT.py:60) regrouped.
+// One wave per hub row; the segment loop is short (<= a few hundred).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_edge_merge(
+    const int* __restrict__ hub_rows, const int* __restrict__ vptr, int n_hub,
+    const float* __restrict__ st_acc, int ld_st, const float* __restrict__ st_ml, int H, int F,
+    int HF, int concat, const float* __restrict__ bias, float* __restrict__ out, int ld_out,
+    float* __restrict__ lse, float* __restrict__ y_heads) {
+    __shared__ float Ms[GAT_MAX_HEADS], Ls[GAT_MAX_HEADS], ys[GAT_MAX_HF];
+    const int k = blockIdx.x;
+    if (k >= n_hub) return;
+    const int lane = threadIdx.x;
+    const int r = hub_rows[k], s0 = vptr[k], s1 = vptr[k + 1];
+    for (int h = lane; h < H; h += kWave) {
+        float M = -INFINITY;
+        for (int sg = s0; sg < s1; ++sg) M = fmaxf(M, st_ml[(size_t)sg * 2 * H + h]);
+        float L = 0.f;
+        for (int sg = s0; sg < s1; ++sg) {
+            const float ms = st_ml[(size_t)sg * 2 * H + h];
+            if (ms != -INFINITY) L += st_ml[(size_t)sg * 2 * H + H + h] * __builtin_amdgcn_exp2f(ms - M);
+        }
+        Ms[h] = M;
+        Ls[h] = L;
+        if (lse != nullptr) lse[(size_t)r * H + h] = (M + log2f(L)) * kLn2;
+    }
+    __syncthreads();
+    for (int cc = lane; cc < HF; cc += kWave) {
+        const int h = cc / F;
+        const float M = Ms[h];
+        float a = 0.f;
+        for (int sg = s0; sg < s1; ++sg) {
+            const float ms = st_ml[(size_t)sg * 2 * H + h];
+            if (ms != -INFINITY) a += st_acc[(size_t)sg * ld_st + cc] * __builtin_amdgcn_exp2f(ms - M);
+        }
+        const float y = a / (Ls[h] + 1e-16f);
+        if (y_heads != nullptr) y_heads[(size_t)r * HF + cc] = y;
+        if (concat) out[(size_t)r * ld_out + cc] = y + bias[cc];
+        else ys[cc] = y;
+    }
+    if (!concat) {
+        __syncthreads();
+        for (int f = lane; f < F; f += kWave) {
+            float sum = 0.f;
+            for (int h = 0; h < H; ++h) sum += ys[h * F + f];
+            out[(size_t)r * ld_out + f] = sum / (float)H + bias[f];
         }
     }
 }
@@ -1827,8 +1531,8 @@ __global__ __launch_bounds__(256) void k_edge_bwd_grp(
 #pragma unroll
     for (int t = 0; t < CL; ++t) {
         const int kk = min(e0 + c + t * G, e1 - 1);
-        cv[t] = col[kk];
-        sv[t] = csr_to_csc[kk];
+        cv[t] = e1 > e0 ? col[kk] : 0;
+        sv[t] = e1 > e0 ? csr_to_csc[kk] : 0;
     }
     for (int k = e0; k < e1; k += U) {
         const int nk = min(U, e1 - k);
@@ -1935,7 +1639,7 @@ __global__ __launch_bounds__(256) void k_bwd_targets(
     float dsd = 0.f;
     int cv[CL];
 #pragma unroll
-    for (int t = 0; t < CL; ++t) cv[t] = col[min(e0 + c + t * G, e1 - 1)];
+    for (int t = 0; t < CL; ++t) cv[t] = e1 > e0 ? col[min(e0 + c + t * G, e1 - 1)] : 0;
     for (int k = e0; k < e1; k += U) {
         const int nk = min(U, e1 - k);
         int cn[CL];
@@ -2402,21 +2106,47 @@ inline int grid_for(long long work, int block, int cap = 256 * 16) {
 
 int status_of(hipError_t e) { return e == hipSuccess ? GAT_OK : (int)e; }
 
-// Kernel-choice knobs for A/B measurement (not part of the ABI): the
-// specialised kernel is the default wherever the shape allows it.
-bool kernel_choice(const char* env, const char* fast, const char* slow) {
-    const char* v = std::getenv(env);
-    if (v == nullptr) return true;
-    if (std::strcmp(v, slow) == 0) return false;
-    (void)fast;
-    return true;
+// Kernel-choice knobs for A/B measurement (tools/, tests; not part of the
+// ABI).  The environment is read ONCE, at the first launch, into a snapshot;
+// gat_tuning_reload() re-reads it (for the tools and tests that switch
+// variants within one process).  The specialised kernels are the default
+// wherever the shape allows them.
+const char* const kKnobNames[] = {
+    "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_EDGE_LDS",  "GAT_EDGE_V",   "GAT_EDGE_U",
+    "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
+    "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG"};
+constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
+
+struct KnobSnapshot {
+    bool set[kNumKnobs];
+    char val[kNumKnobs][32];
+};
+KnobSnapshot g_knobs;
+bool g_knobs_ready = false;
+
+void snapshot_knobs() {
+    for (int i = 0; i < kNumKnobs; ++i) {
+        const char* v = std::getenv(kKnobNames[i]);
+        g_knobs.set[i] = v != nullptr;
+        g_knobs.val[i][0] = '\0';
+        if (v != nullptr) {
+            std::strncpy(g_knobs.val[i], v, sizeof(g_knobs.val[i]) - 1);
+            g_knobs.val[i][sizeof(g_knobs.val[i]) - 1] = '\0';
+        }
+    }
+    g_knobs_ready = true;
 }
 
-int edge_unroll() {
-    const char* v = std::getenv("GAT_EDGE_U");
-    if (v == nullptr) return 8;
-    const int u = std::atoi(v);
-    return (u == 4 || u == 16) ? u : 8;
+const char* knob(const char* name) {
+    if (!g_knobs_ready) snapshot_knobs();
+    for (int i = 0; i < kNumKnobs; ++i)
+        if (std::strcmp(kKnobNames[i], name) == 0) return g_knobs.set[i] ? g_knobs.val[i] : nullptr;
+    return nullptr;
+}
+
+bool kernel_choice(const char* env, const char* slow) {
+    const char* v = knob(env);
+    return !(v != nullptr && std::strcmp(v, slow) == 0);
 }
 
 }  // namespace
@@ -2427,6 +2157,11 @@ int edge_unroll() {
 extern "C" {
 
 int gat_abi_version(void) { return GAT_ABI_VERSION; }
+
+int gat_tuning_reload(void) {
+    snapshot_knobs();
+    return GAT_OK;
+}
 
 int gat_table_layout(int heads, int f, int* ld, int* s_off) {
     if (heads <= 0 || f <= 0 || ld == nullptr || s_off == nullptr) return GAT_EINVAL;
@@ -2460,57 +2195,24 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
     const int nt = (hf + 15) / 16;
-    // GAT_PROJ_KERNEL (A/B knob): "wk" (default for fin <= 128: whole K in LDS),
-    // "tiled" (K-tiled, shuffle epilogue; default for larger fin), "lds"
-    // (K-tiled, LDS epilogue), "direct" (register-direct, F a power of two)
-    const char* pk = sliced ? nullptr : std::getenv("GAT_PROJ_KERNEL");
+    // GAT_PROJ_KERNEL (A/B knob, tools/tests): "wk" (whole K in LDS; the
+    // default for fin <= 64), "pipe" (pipelined K loop; the default for larger
+    // fin), "tiled" / "lds" (K-tiled fallback, shuffle / LDS epilogue)
+    const char* pk = sliced ? nullptr : knob("GAT_PROJ_KERNEL");
     const bool pow2_f = next_pow2(f) == f;
     const size_t wk_lds = (size_t)wk_lds_floats(fin, nt) * sizeof(float);
-    const size_t wk_out = 0;  // the output tile is inside wk_lds_floats
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) |
                              reinterpret_cast<uintptr_t>(wh)) & 15) == 0;
     int wk_max = 64;  // GAT_PROJ_WK_MAX (A/B knob): largest fin for the whole-K kernel
-    if (const char* v = std::getenv("GAT_PROJ_WK_MAX")) wk_max = std::atoi(v);
-    // persistent, tile-pipelined kernel: opt-in only (GAT_PROJ_KERNEL=persist).
-    // Measured slower than k_project_wk at PPI shape (16.2 vs 12.7 us hot, 21.7
-    // vs 16.7 us after the edge kernel): 2 blocks/CU keep too few loads in flight
-    const bool persist_ok = fin > 0 && fin <= 64 && nt <= 4 && n >= 64 && aligned16 &&
-                            pk != nullptr && std::strcmp(pk, "persist") == 0;
-    if (persist_ok) {
-        static int cus = 0;
-        if (cus == 0) {
-            int dev = 0, v = 0;
-            if (hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-                cus = v;
-            if (cus <= 0) cus = 256;
-        }
-        const int ntiles = (n + 63) / 64;
-        const int blocks = ntiles < 2 * cus ? ntiles : 2 * cus;
-        const size_t lds = (size_t)persist_lds_floats(fin, nt) * sizeof(float);
-#define GAT_PERSIST_CASE(NT)                                                                  \
-    case NT:                                                                                  \
-        hipLaunchKernelGGL((k_project_persist<NT>), dim3(blocks), dim3(256), lds, st, x, n,    \
-                           fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh,    \
-                           s_src, ld_s, s_dst);                                               \
-        break;
-        switch (nt) {
-            GAT_PERSIST_CASE(1) GAT_PERSIST_CASE(2) GAT_PERSIST_CASE(3) GAT_PERSIST_CASE(4)
-            default: return GAT_EUNSUPPORTED;
-        }
-#undef GAT_PERSIST_CASE
-        return status_of(hipGetLastError());
-    }
-    const bool wk_ok = fin > 0 && fin <= wk_max && aligned16 &&
-                       (wk_lds > wk_out ? wk_lds : wk_out) <= 160 * 1024 &&
+    if (const char* v = knob("GAT_PROJ_WK_MAX")) wk_max = std::atoi(v);
+    const bool wk_ok = fin > 0 && fin <= wk_max && aligned16 && wk_lds <= 160 * 1024 &&
                        (pk == nullptr || std::strcmp(pk, "wk") == 0);
     if (wk_ok) {
-        const size_t lds = wk_lds > wk_out ? wk_lds : wk_out;
 #define GAT_WK_CASE(NT)                                                                       \
     case NT:                                                                                  \
-        hipLaunchKernelGGL((k_project_wk<NT>), grid, block, lds, st, x, n, fin, w, b, a_src,  \
-                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
-                           slice_w, slice_stride);                                            \
+        hipLaunchKernelGGL((k_project_wk<NT>), grid, block, wk_lds, st, x, n, fin, w, b,      \
+                           a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s,  \
+                           s_dst, slice_w, slice_stride);                                     \
         break;
         switch (nt) {
             GAT_WK_CASE(1) GAT_WK_CASE(2) GAT_WK_CASE(3) GAT_WK_CASE(4)
@@ -2522,20 +2224,16 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #undef GAT_WK_CASE
         return status_of(hipGetLastError());
     }
-    // pipelined K loop for large fin (F a power of two dividing 16, HF <= 64);
-    // GAT_PROJ_KERNEL=tiled keeps the K-tiled kernel (A/B knob)
+    // pipelined K loop for large fin (F a power of two dividing 16, HF in
+    // {16, 32, 64}, i.e. nt in {1, 2, 4}); LW floats per lane where fin allows
     const bool force_pipe = pk != nullptr && std::strcmp(pk, "pipe") == 0;
-    const bool pipe_ok = (fin > 64 || force_pipe) && fin > 0 && nt <= 4 && pow2_f && f <= 16 &&
+    const bool pipe_ok = (fin > 64 || force_pipe) && fin > 0 &&
+                         (nt == 1 || nt == 2 || nt == 4) && pow2_f && f <= 16 &&
                          (long long)n * fin < (1LL << 31) && (pk == nullptr || force_pipe);
     if (pipe_ok) {
         const dim3 gp((n + 127) / 128), bp(256);
-        // vector-width variant (k_project_pipe2; GAT_PROJ_PIPE=1 keeps the
-        // one-float-per-lane kernel): LW floats per lane where fin allows
-        const char* pv = std::getenv("GAT_PROJ_PIPE");
-        const bool pipe2 = (nt == 1 || nt == 2 || nt == 4) && !(pv && std::atoi(pv) == 1);
-        if (pipe2) {
-            const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
-            const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
+        const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
+        const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
 #define GAT_PIPE2(NT, LWV)                                                                     \
     hipLaunchKernelGGL((k_project_pipe2<NT, LWV>), gp, bp, 0, st, x, n, fin, w, b, a_src,     \
                        c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,      \
@@ -2544,47 +2242,14 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     if (lw == 4) { GAT_PIPE2(NT, 4); }                    \
     else if (lw == 2) { GAT_PIPE2(NT, 2); }               \
     else { GAT_PIPE2(NT, 1); }
-            if (nt == 1) { GAT_PIPE2_LW(1) }
-            else if (nt == 2) { GAT_PIPE2_LW(2) }
-            else { GAT_PIPE2_LW(4) }
+        if (nt == 1) { GAT_PIPE2_LW(1) }
+        else if (nt == 2) { GAT_PIPE2_LW(2) }
+        else { GAT_PIPE2_LW(4) }
 #undef GAT_PIPE2_LW
 #undef GAT_PIPE2
-            return status_of(hipGetLastError());
-        }
-#define GAT_PIPE_CASE(NT)                                                                     \
-    case NT:                                                                                  \
-        hipLaunchKernelGGL((k_project_pipe<NT>), gp, bp, 0, st, x, n, fin, w, b, a_src, c_src, \
-                           a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,         \
-                           slice_w, slice_stride);                                            \
-        break;
-        switch (nt) {
-            GAT_PIPE_CASE(1) GAT_PIPE_CASE(2) GAT_PIPE_CASE(3) GAT_PIPE_CASE(4)
-            default: return GAT_EUNSUPPORTED;
-        }
-#undef GAT_PIPE_CASE
         return status_of(hipGetLastError());
     }
     if (sliced) return GAT_EUNSUPPORTED;  // the kernels below write row-major Wh only
-    if (pow2_f && pk != nullptr && std::strcmp(pk, "direct") == 0) {
-        int tw = nt < 2 ? nt : 2;
-        if (f / 16 > tw) tw = f / 16;
-        const int cgroups = (nt + tw - 1) / tw;
-        const long long waves = (long long)((n + 15) / 16) * cgroups;
-        const dim3 gd((unsigned)((waves + 3) / 4)), bd(256);
-#define GAT_PD(TW)                                                                             \
-    hipLaunchKernelGGL((k_project_direct<TW>), gd, bd, 0, st, x, n, fin, w, b, a_src, c_src,    \
-                       a_dst, c_dst, heads, f, hf, cgroups, wh, ld_wh, s_src, ld_s, s_dst)
-        switch (tw) {
-            case 1: GAT_PD(1); break;
-            case 2: GAT_PD(2); break;
-            case 4: GAT_PD(4); break;
-            case 8: GAT_PD(8); break;
-            case 16: GAT_PD(16); break;
-            default: return GAT_EUNSUPPORTED;
-        }
-#undef GAT_PD
-        return status_of(hipGetLastError());
-    }
     const bool shfl = ((f <= 16 && 16 % f == 0) || (f % 16 == 0)) &&
                       !(pk != nullptr && std::strcmp(pk, "lds") == 0);
 #define GAT_PROJ_CASE(NT)                                                                   \
@@ -2637,7 +2302,7 @@ static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A
     // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
     // kernel — caps the blocks resident per CU (160 KB / bytes)
     size_t lds = 0;
-    if (const char* el = std::getenv("GAT_EDGE_LDS")) lds = (size_t)std::atol(el);
+    if (const char* el = knob("GAT_EDGE_LDS")) lds = (size_t)std::atol(el);
     if constexpr ((V == 1 && (U == 4 || U == 8)) || (V == 2 && (U == 8 || U == 16))) {
         if (pipe) {
             hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true>), grid, block, lds, st, a...);
@@ -2649,7 +2314,7 @@ static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A
 
 extern "C" {
 
-static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row_order,
+static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row_order,
                                int row_begin, int row_end, const float* wh, int ld_wh,
                                const float* s_src, int ld_s, const float* a_src,
                                const float* c_src, const float* s_dst, int heads, int f,
@@ -2691,7 +2356,7 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
     // twice the rows per wave (tools/tune_edge.py: Reddit 3.34 -> 3.23 ms; PPI and
     // arxiv are no faster with V = 2)
     int vv = edges_per_row_hint >= 128 ? 2 : 1;
-    if (const char* ev = std::getenv("GAT_EDGE_V")) vv = std::atoi(ev);
+    if (const char* ev = knob("GAT_EDGE_V")) vv = std::atoi(ev);
     if (vv != 1 && vv != 2 && vv != 4) vv = 1;
 
     while (vv > 1 && f % (4 * vv) != 0) vv >>= 1;
@@ -2702,17 +2367,17 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
     const bool grp_ok = (f % 4 == 0) && (concat || pow2_hl) && slope_ok;
     // fused source score: the head's lanes must form an aligned power-of-two block
     bool fused = grp_ok && pow2_hl && have_a;
-    if (fused && s_src != nullptr) fused = kernel_choice("GAT_EDGE_SCORE", "fused", "gather");
+    if (fused && s_src != nullptr) fused = kernel_choice("GAT_EDGE_SCORE", "gather");
     if (s_src == nullptr && !fused) return GAT_EUNSUPPORTED;
     // a slice holds whole heads (the fused score sums a head inside one group)
     if (sliced && (!fused || slice_w % f != 0)) return GAT_EUNSUPPORTED;
-    if (grp_ok && (s_src == nullptr || kernel_choice("GAT_EDGE_KERNEL", "group", "generic"))) {
+    if (grp_ok && (s_src == nullptr || kernel_choice("GAT_EDGE_KERNEL", "generic"))) {
         // edges per chunk: short rows want short chunks (less padding), long rows
         // more loads in flight; GAT_EDGE_U overrides
         // (tools/tune_edge.py: PPI, ~28 per row, 36.9 us at U = 8 -> 33.1 us at U = 4)
         int u = edges_per_row_hint <= 0 ? 8 : edges_per_row_hint <= 32 ? 4
               : edges_per_row_hint <= 64 ? 8 : 16;
-        if (const char* eu = std::getenv("GAT_EDGE_U")) u = std::atoi(eu);
+        if (const char* eu = knob("GAT_EDGE_U")) u = std::atoi(eu);
         const long long threads = (long long)rows * g;
         const long long blocks = ((threads + 255) / 256) * nslices;
         if (blocks >= (1LL << 31)) return GAT_EUNSUPPORTED;
@@ -2722,9 +2387,9 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
         // lane; tools/slice_probe.py, Reddit scale 2.60 -> 1.99 ms); shorter
         // rows keep more, shallower waves (PPI 30.5 -> 32.9 us pipelined)
         int pipe = (u == 16 && vv == 2) ? 1 : 0;
-        if (const char* ep = std::getenv("GAT_EDGE_PIPE")) pipe = std::atoi(ep);
+        if (const char* ep = knob("GAT_EDGE_PIPE")) pipe = std::atoi(ep);
 #define GAT_GRP_KARGS                                                                         \
-    rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,   \
+    er, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,   \
         heads, f, hf, concat, negative_slope, bias, out, ld_out, lse, drop, y_heads, nslices,  \
         slice_w, slice_stride
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
@@ -2756,6 +2421,9 @@ static int edge_aggregate_impl(const int* rowptr, const int* col, const int* row
 #undef GAT_GRP_KARGS
         return status_of(hipGetLastError());
     }
+    // the generic kernel runs whole CSR rows only
+    if (er.by_pos || er.load || er.store_lt > 0 || er.ee != er.eb + 1) return GAT_EUNSUPPORTED;
+    const int* rowptr = er.eb;
     const int lpe = next_pow2((round_up4(hf) + 3) / 4);
     const int hp = next_pow2(heads);
     const dim3 grid(rows), block(kWave);
@@ -2795,7 +2463,7 @@ int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, 
                        const float* a_src, const float* c_src, const float* s_dst, int heads,
                        int f, int concat, float negative_slope, const float* bias, float* out,
                        float* lse, int edges_per_row_hint, void* stream) {
-    return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src,
+    return edge_aggregate_impl(rows_of_csr(rowptr), col, row_order, row_begin, row_end, wh, ld_wh, s_src,
                                ld_s, a_src, c_src, s_dst, heads, f, concat, GAT_ACT_LEAKY_RELU,
                                negative_slope, bias, out, lse, nullptr, make_drop(0.f, 0ull),
                                edges_per_row_hint, stream);
@@ -2811,7 +2479,7 @@ int gat_edge_aggregate_sliced(const int* rowptr, const int* col, const int* row_
         return GAT_EINVAL;
     if (a_src == nullptr || c_src == nullptr) return GAT_EINVAL;
     const int sw = heads * f / slices;
-    return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, sw, nullptr, 0,
+    return edge_aggregate_impl(rows_of_csr(rowptr), col, row_order, row_begin, row_end, wh, sw, nullptr, 0,
                                a_src, c_src, s_dst, heads, f, 1, GAT_ACT_LEAKY_RELU,
                                negative_slope, bias, out, nullptr, nullptr, make_drop(0.f, 0ull),
                                edges_per_row_hint, stream, slices, (long long)n_table * sw);
@@ -2825,10 +2493,67 @@ int gat_edge_aggregate_ex(const int* rowptr, const int* col, const int* row_orde
                           const float* bias, float* out, float* lse, float* y_heads,
                           int edges_per_row_hint, void* stream) {
     if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
-    return edge_aggregate_impl(rowptr, col, row_order, row_begin, row_end, wh, ld_wh, s_src,
+    return edge_aggregate_impl(rows_of_csr(rowptr), col, row_order, row_begin, row_end, wh, ld_wh, s_src,
                                ld_s, a_src, c_src, s_dst, heads, f, concat, score_act, act_param,
                                bias, out, lse, y_heads, make_drop(dropout_p, seed, seed_dev),
                                edges_per_row_hint, stream);
+}
+
+int gat_edge_aggregate_seg(const int* seg_begin, const int* seg_end, int seg_by_pos,
+                           const int* col, const int* row_order, int row_begin, int row_end,
+                           const float* wh, int ld_wh, int n_table, int slices,
+                           const float* a_src, const float* c_src, const float* s_dst, int heads,
+                           int f, int concat, float negative_slope, float* st_acc, float* st_ml,
+                           int flags, int store_rows, const float* bias, float* out,
+                           int edges_per_row_hint, void* stream) {
+    if (seg_begin == nullptr || seg_end == nullptr || a_src == nullptr || c_src == nullptr)
+        return GAT_EINVAL;
+    if (heads <= 0 || f <= 0 || slices <= 0 || (flags & ~(GAT_SEG_LOAD | GAT_SEG_STORE)))
+        return GAT_EINVAL;
+    const int hf = heads * f;
+    if ((flags != 0) && (st_acc == nullptr || st_ml == nullptr)) return GAT_EINVAL;
+    EdgeRows er;
+    er.eb = seg_begin;
+    er.ee = seg_end;
+    er.st_acc = st_acc;
+    er.st_ml = st_ml;
+    er.ld_st = round_up4(hf);
+    er.by_pos = seg_by_pos != 0;
+    er.load = (flags & GAT_SEG_LOAD) != 0;
+    // GAT_SEG_STORE: every row stores its state; else, by position, the rows at
+    // positions < store_rows do (split hub segments ahead of whole rows)
+    er.store_lt = (flags & GAT_SEG_STORE) ? 0x7fffffff : (seg_by_pos ? store_rows : 0);
+    if (store_rows < 0 || (store_rows > 0 && !seg_by_pos)) return GAT_EINVAL;
+    if (er.store_lt > 0 && (st_acc == nullptr || st_ml == nullptr)) return GAT_EINVAL;
+    if (slices > 1) {
+        if (n_table <= 0 || hf % slices != 0) return GAT_EINVAL;
+        const int sw = hf / slices;
+        return edge_aggregate_impl(er, col, row_order, row_begin, row_end, wh, sw, nullptr, 0,
+                                   a_src, c_src, s_dst, heads, f, concat, GAT_ACT_LEAKY_RELU,
+                                   negative_slope, bias, out, nullptr, nullptr,
+                                   make_drop(0.f, 0ull), edges_per_row_hint, stream, slices,
+                                   (long long)n_table * sw);
+    }
+    return edge_aggregate_impl(er, col, row_order, row_begin, row_end, wh, ld_wh, nullptr, 0,
+                               a_src, c_src, s_dst, heads, f, concat, GAT_ACT_LEAKY_RELU,
+                               negative_slope, bias, out, nullptr, nullptr, make_drop(0.f, 0ull),
+                               edges_per_row_hint, stream);
+}
+
+int gat_edge_merge(const int* hub_rows, const int* seg_ptr, int n_hub, const float* st_acc,
+                   const float* st_ml, int heads, int f, int concat, const float* bias,
+                   float* out, float* lse, float* y_heads, void* stream) {
+    if (heads <= 0 || f <= 0 || n_hub < 0) return GAT_EINVAL;
+    const int hf = heads * f;
+    if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
+    if (n_hub == 0) return GAT_OK;
+    if (hub_rows == nullptr || seg_ptr == nullptr || st_acc == nullptr || st_ml == nullptr ||
+        bias == nullptr || out == nullptr)
+        return GAT_EINVAL;
+    hipLaunchKernelGGL(k_edge_merge, dim3(n_hub), dim3(kWave), 0, (hipStream_t)stream, hub_rows,
+                       seg_ptr, n_hub, st_acc, round_up4(hf), st_ml, heads, f, hf, concat, bias,
+                       out, concat ? hf : f, lse, y_heads);
+    return status_of(hipGetLastError());
 }
 
 size_t csr_key_sort_tmp_bytes(long long nnz, int n) {
@@ -2963,13 +2688,13 @@ int gat_bwd_table_layout(int heads, int f, int concat, int* ld_t) {
 // GAT_BWD_LDS (A/B knob): dynamic LDS bytes per block for the recompute
 // backward kernels, unused by them — caps the blocks resident per CU
 static size_t bwd_lds_bytes() {
-    const char* v = std::getenv("GAT_BWD_LDS");
+    const char* v = knob("GAT_BWD_LDS");
     return v != nullptr ? (size_t)std::atol(v) : 0;
 }
 
 static int bwd_unroll(int hint) {
     int u = hint <= 0 ? 8 : hint <= 32 ? 4 : hint <= 64 ? 8 : 16;
-    if (const char* v = std::getenv("GAT_BWD_U")) {
+    if (const char* v = knob("GAT_BWD_U")) {
         const int x = std::atoi(v);
         u = (x == 4 || x == 16) ? x : 8;
     }
@@ -2978,7 +2703,7 @@ static int bwd_unroll(int hint) {
 
 static bool bwd_recompute_ok(int heads, int f, float slope, const float* wh, int ld_wh) {
     // GAT_BWD_KERNEL=stored|generic (A/B knob): force the stored-coefficient path
-    if (const char* v = std::getenv("GAT_BWD_KERNEL"))
+    if (const char* v = knob("GAT_BWD_KERNEL"))
         if (std::strcmp(v, "stored") == 0 || std::strcmp(v, "generic") == 0) return false;
     const int hl = f / 4;
     return heads * f <= GAT_MAX_HF && heads <= GAT_MAX_HEADS && f % 4 == 0 &&
@@ -3034,7 +2759,7 @@ int gat_bwd_sources_parts(int num_nodes, int heads, int f, int* num_parts) {
     const int g = next_pow2((heads * f + 3) / 4);
     const long long waves = ((long long)num_nodes * g + kWave - 1) / kWave;
     long long cap = 65536;  // GAT_BWD_WAVES overrides (A/B knob)
-    if (const char* v = std::getenv("GAT_BWD_WAVES")) cap = std::atoll(v) > 0 ? std::atoll(v) : cap;
+    if (const char* v = knob("GAT_BWD_WAVES")) cap = std::atoll(v) > 0 ? std::atoll(v) : cap;
     long long w = waves < cap ? waves : cap;
     w = (w + 3) / 4 * 4;  // whole 256-thread blocks
     *num_parts = (int)(w < 4 ? 4 : w);
@@ -3103,7 +2828,7 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
     const bool grp_ok = score_act == GAT_ACT_LEAKY_RELU && act_param >= 0.f && act_param <= 1.f &&
                         f % 4 == 0 && next_pow2(hl) == hl && a_src != nullptr &&
                         c_src != nullptr && (ld_wh & 3) == 0 &&
-                        kernel_choice("GAT_BWD_KERNEL", "group", "generic");
+                        kernel_choice("GAT_BWD_KERNEL", "generic");
     if (grp_ok) {
         const int g = next_pow2(hf / 4);
         const int u = edges_per_row_hint > 0 && edges_per_row_hint <= 12 ? 4 : 8;

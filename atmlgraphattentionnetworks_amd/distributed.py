@@ -5,21 +5,32 @@ distributed code to mirror.  This is the scaling axis SURVEY.md §8e defines:
 
 * target rows are split into P contiguous ranges, edge-balanced by a prefix
   sum over ``rowptr`` (each rank gets ~E'/P in-edges, not N/P rows);
-* each rank projects its own rows (``gat_project``) into its slot of a padded
-  node table [P * M, ld] (M = the largest range), then ONE RCCL all-gather
-  (``all_gather_into_tensor``, in place) fills every other slot over xGMI —
-  Wh and s_src travel together in the packed table row;
-* each rank runs the edge kernel over its own rows; col ids were remapped
-  once, at setup, from global node ids to table rows (p * M + local);
+* each rank projects its own rows (``gat_project``) into its slots of ONE
+  node table that every rank holds, and an RCCL all-gather over xGMI fills
+  the other ranks' slots;
+* each rank runs the edge kernel over its own target rows; source ids were
+  remapped once, at setup, from global node ids to table rows;
 * outputs stay sharded; ``gather_output`` concatenates them for checks.
+
+Overlap.  The table is laid out in K CHUNKS, [K][P][S planes][B rows][W]:
+chunk c holds rows [c*B, (c+1)*B) of every rank.  A step issues, per chunk,
+the projection of the rank's rows of that chunk and then an asynchronous
+in-place ``all_gather_into_tensor`` of the chunk (RCCL runs it on its own
+stream); the edge work then runs as K passes, pass c over the in-edges whose
+sources lie in chunk c (each row's sources are sorted by table row, so they
+form one contiguous segment), carrying the online-softmax state (m, l, acc)
+from pass to pass (``gat_edge_aggregate_seg``).  Pass c waits only for chunk
+c, so the all-gather of chunks c+1.. proceeds under pass c.  K = 1 is the
+plain project -> all-gather -> edge kernel step.
 
 ``exchange="replicate"`` is the alternative SURVEY.md §8e lists: every rank
 holds all of x and recomputes the full projection, so there is no
 collective in the step at all.
 
-The compute ops are pluggable (``ops``) so the partition / remap / all-gather
-logic can be exercised on CPU with gloo (tests/test_distributed_gloo.py);
-the default ops are the HIP kernels.
+The compute ops are pluggable (``ops``) so the partition / remap / chunk /
+segment logic runs on CPU under gloo (tests/test_distributed_gloo.py); the
+default ops are the HIP kernels, and the one-GPU emulation (``emulate``)
+runs them for P virtual ranks (tests/test_gpu_distributed.py).
 """
 from __future__ import annotations
 
@@ -28,11 +39,12 @@ import os
 import sys
 import time
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
+from . import _lib
 
 
 def partition_rows(rowptr: torch.Tensor, parts: int) -> List[int]:
@@ -49,74 +61,215 @@ def partition_rows(rowptr: torch.Tensor, parts: int) -> List[int]:
     return bounds
 
 
-@dataclass
-class LocalCSR:
-    rowptr: torch.Tensor  # int32 [n_local + 1], starts at 0
-    col: torch.Tensor  # int32 table-row ids
-    num_nodes: int  # n_local rows
-    num_edges: int
-    order: Optional[torch.Tensor] = None  # int32 [n_local], rows by descending in-degree
-
-
 def degree_order(rowptr: torch.Tensor) -> torch.Tensor:
-    """Rows by descending in-degree, stable (the same schedule gat_csr_build emits)."""
+    """Rows by descending in-degree, stable (the schedule gat_csr_build emits)."""
     deg = (rowptr[1:] - rowptr[:-1]).to(torch.int64)
     return torch.argsort(deg, descending=True, stable=True).to(torch.int32)
 
 
-def remap_to_table(col: torch.Tensor, bounds: List[int], rows_per_part: int) -> torch.Tensor:
-    """Global node id -> row of the padded, all-gathered table (p * M + local)."""
-    b = torch.tensor(bounds, dtype=torch.int64, device=col.device)
-    c = col.to(torch.int64)
-    part = torch.searchsorted(b[1:], c, right=True)
-    return (part * rows_per_part + (c - b[part])).to(torch.int32)
+@dataclass(frozen=True)
+class TableLayout:
+    """The node table every rank holds: [chunks][world][slices][block_rows][width]
+    fp32.  ``kind``: "planes" (Wh as column planes, the eval forward's layout),
+    "wh" (row-major Wh only: the edge kernel recomputes s_src from the row) or
+    "packed" ([Wh | s_src] rows, for score activations the fused kernels do not
+    take).  A node's table row is its plane-0 row index:
+    (c * world + p) * slices * block_rows + i for the i-th row of rank p's
+    chunk c; plane g of it lies g * block_rows rows further (the kernels'
+    plane stride n_table = block_rows)."""
+    kind: str
+    world: int
+    chunks: int
+    block_rows: int
+    slices: int
+    width: int
+    s_off: int = 0
+
+    @property
+    def block_floats(self) -> int:
+        return self.slices * self.block_rows * self.width
+
+    @property
+    def numel(self) -> int:
+        return self.chunks * self.world * self.block_floats
+
+    @property
+    def table_rows(self) -> int:
+        return self.chunks * self.world * self.slices * self.block_rows
+
+    def block_offset(self, c: int, p: int) -> int:
+        return (c * self.world + p) * self.block_floats
+
+    def chunk_range(self, c: int):
+        per = self.world * self.block_floats
+        return c * per, (c + 1) * per
+
+    def row_of(self, part: torch.Tensor, local: torch.Tensor) -> torch.Tensor:
+        c = torch.div(local, self.block_rows, rounding_mode="floor")
+        i = local - c * self.block_rows
+        return (c * self.world + part) * (self.slices * self.block_rows) + i
+
+    def chunk_of_row(self, trow: torch.Tensor) -> torch.Tensor:
+        return torch.div(trow, self.world * self.slices * self.block_rows, rounding_mode="floor")
+
+
+@dataclass
+class LocalCSR:
+    rowptr: torch.Tensor  # int32 [n_local + 1], starts at 0
+    col: torch.Tensor  # int32 table rows, ascending within each row
+    num_nodes: int  # n_local rows
+    num_edges: int
+    order: Optional[torch.Tensor] = None  # int32 [n_local], rows by descending in-degree
+    seg: Optional[torch.Tensor] = None  # int32 [chunks + 1, n_local]: pass c = [seg[c], seg[c+1])
+
+
+def _score(layer):
+    """(activation code, parameter) of the layer's score activation."""
+    act = getattr(layer, "score_activation", None)
+    if act is None:
+        return _lib.GAT_ACT_LEAKY_RELU, 0.2  # test stand-ins: the reference default
+    return act()
+
+
+def fused_score_ok(heads: int, f: int, act: int, param: float) -> bool:
+    """The fused-score kernels (Wh-only / planes tables, segmented passes):
+    LeakyReLU with slope in [0, 1], f % 4 == 0 and f/4 a power of two."""
+    hl = f // 4
+    return (act == _lib.GAT_ACT_LEAKY_RELU and 0.0 <= param <= 1.0 and f % 4 == 0 and hl > 0
+            and (hl & (hl - 1)) == 0)
+
+
+def default_chunks(world: int, local_edges: int, fused: bool) -> int:
+    """All-gather chunks (= edge passes) per step: one pass per ~4M local edges,
+    at most 4; 1 on a single rank or without the fused kernels."""
+    if world <= 1 or not fused:
+        return 1
+    return max(1, min(4, local_edges // 4_000_000))
 
 
 class HipOps:
     """The HIP kernels (default)."""
 
     @staticmethod
-    def alloc_table(n, heads, f, device, packed=True, wh_only=False, slices=1):
-        from .layer import alloc_table
-        if slices > 1:
-            return alloc_table(n, heads, f, device, slices=slices)
-        return alloc_table(n, heads, f, device, packed=packed, wh_only=wh_only)
+    def project_rows(x, pp, heads, f, layout: TableLayout, table, offset, s_dst, s_scratch):
+        """Project rows x into the table block at float offset ``offset``."""
+        lib = _lib.load()
+        n, fin = x.shape
+        if n == 0:
+            return
+        stream = torch._C._cuda_getCurrentRawStream(x.device.index)
+        wh = table.data_ptr() + 4 * offset
+        args = (x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(),
+                pp.c_src.data_ptr(), pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f)
+        if layout.kind == "planes":
+            rc = lib.gat_project_sliced(*args, layout.slices, wh, layout.block_rows, 0, heads,
+                                        s_dst.data_ptr(), stream)
+        elif layout.kind == "wh":
+            rc = lib.gat_project(*args, wh, layout.width, s_scratch.data_ptr(), heads,
+                                 s_dst.data_ptr(), stream)
+        else:
+            rc = lib.gat_project(*args, wh, layout.width, wh + 4 * layout.s_off, layout.width,
+                                 s_dst.data_ptr(), stream)
+        _lib.check(rc, "gat_project (shard block)")
 
     @staticmethod
-    def project(x, pp, heads, f, table, s_dst):
-        from .layer import project
-        return project(x, pp, heads, f, table=table, s_dst=s_dst)
+    def edge_pass(local: LocalCSR, c: int, layout: TableLayout, table, s_dst, pp, bias, heads,
+                  f, concat, act, param, out, st_acc, st_ml, flags):
+        lib = _lib.load()
+        n = local.num_nodes
+        if n == 0:
+            return out
+        stream = torch._C._cuda_getCurrentRawStream(table.device.index)
+        hint = local.num_edges // max(n, 1)
+        order = 0 if local.order is None else local.order.data_ptr()
+        if layout.kind == "packed":
+            if flags:
+                raise ValueError("the packed table runs one pass")
+            rc = lib.gat_edge_aggregate_ex(
+                local.rowptr.data_ptr(), local.col.data_ptr(), order, 0, n, table.data_ptr(),
+                layout.width, table.data_ptr() + 4 * layout.s_off, layout.width, 0, 0,
+                s_dst.data_ptr(), heads, f, int(concat), act, float(param), 0.0, 0, 0,
+                bias.data_ptr(), out.data_ptr(), 0, 0, hint, stream)
+            _lib.check(rc, "gat_edge_aggregate_ex (shard)")
+            return out
+        sb = local.seg[c].data_ptr()
+        se = local.seg[c + 1].data_ptr()
+        rc = lib.gat_edge_aggregate_seg(
+            sb, se, 0, local.col.data_ptr(), order, 0, n, table.data_ptr(), layout.width,
+            layout.block_rows, layout.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+            s_dst.data_ptr(), heads, f, int(concat), float(param),
+            0 if st_acc is None else st_acc.data_ptr(), 0 if st_ml is None else st_ml.data_ptr(),
+            flags, 0, bias.data_ptr(), out.data_ptr(), hint, stream)
+        _lib.check(rc, "gat_edge_aggregate_seg (shard pass)")
+        return out
+
+
+class CollectiveExchange:
+    """In-place all-gather of one table chunk over a process group (RCCL for
+    CUDA tensors; gloo for the CPU tests), asynchronous: ``start`` returns the
+    work handle and ``wait`` makes the current stream wait for it."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def start(self, chunk: torch.Tensor, part: torch.Tensor):
+        return dist.all_gather_into_tensor(chunk, part, group=self.group, async_op=True)
 
     @staticmethod
-    def edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope, out, pp=None):
-        from .layer import edge_aggregate
-        return edge_aggregate(csr, table, s_dst, heads, f, concat, bias, negative_slope, out=out,
-                              pp=pp)
+    def wait(handle) -> None:
+        if handle is not None:
+            handle.wait()
 
 
-def _default_score(layer) -> bool:
-    """LeakyReLU score activation with slope in [0, 1] (the fused-score kernels)."""
-    act = getattr(layer, "score_activation", None)
-    if act is None:
-        return True  # layers without the hook (test stand-ins) use the reference default
-    code, param = act()
-    return code == 0 and 0.0 <= param <= 1.0
+class HostStagedExchange:
+    """The same all-gather staged through host memory over a CPU (gloo)
+    group: for rehearsing the multi-process path with several ranks on ONE
+    GPU, where RCCL refuses duplicate devices.  Synchronous."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def start(self, chunk: torch.Tensor, part: torch.Tensor):
+        host = torch.empty(chunk.numel(), dtype=chunk.dtype)
+        dist.all_gather_into_tensor(host, part.cpu(), group=self.group)
+        chunk.copy_(host)
+        return None
+
+    @staticmethod
+    def wait(handle) -> None:
+        return None
+
+
+class NoExchange:
+    """A single rank, or the one-process emulation (``emulate``) that copies
+    the blocks itself."""
+
+    @staticmethod
+    def start(chunk, part):
+        return None
+
+    @staticmethod
+    def wait(handle) -> None:
+        return None
 
 
 class ShardedGAT:
     """One rank's share of a node-range partitioned GAT layer forward."""
 
     def __init__(self, layer, csr, world: int, rank: int, exchange: str = "allgather",
-                 group=None, ops=None, packed=None):
+                 group=None, ops=None, packed=None, chunks: Optional[int] = None,
+                 exchanger=None):
         if exchange not in ("allgather", "replicate"):
             raise ValueError(exchange)
-        self.layer, self.world, self.rank, self.group = layer, world, rank, group
+        self.layer, self.world, self.rank = layer, world, rank
         self.exchange = exchange
         self.ops = ops or HipOps
         self.heads, self.f = layer.num_heads, layer.output_channels
         self.concat = layer.concat
         self.pp = packed if packed is not None else layer.packed()
         self.bias = layer.bias.detach()
+        self.act, self.param = _score(layer)
+        heads, f, hf = self.heads, self.f, self.heads * self.f
         dev = csr.rowptr.device
         self.bounds = partition_rows(csr.rowptr, world)
         self.r0, self.r1 = self.bounds[rank], self.bounds[rank + 1]
@@ -124,91 +277,194 @@ class ShardedGAT:
         self.rows_per_part = max(max(self.bounds[k + 1] - self.bounds[k] for k in range(world)), 1)
         rp = csr.rowptr
         e0, e1 = int(rp[self.r0]), int(rp[self.r1])
-        col = csr.col[e0:e1]
+        self.fused = fused_score_ok(heads, f, self.act, self.param)
+        # table layout: planes where the single-GPU eval forward would use them
+        # (layer.wh_slices), else Wh-only rows, else packed [Wh | s_src]
+        from .layer import wh_slices
+        slices = 1
+        if self.fused:
+            slices = wh_slices(heads, f, self.concat, self.param,
+                               csr.num_edges // max(csr.num_nodes, 1))
+        kind = "planes" if slices > 1 else ("wh" if self.fused else "packed")
+        if kind == "planes":
+            width = hf // slices
+            s_off = 0
+        elif kind == "wh":
+            width = (hf + 3) // 4 * 4
+            s_off = 0
+        else:
+            width, s_off = _lib.table_layout(heads, f)
         if exchange == "allgather":
-            col = remap_to_table(col, self.bounds, self.rows_per_part)
-            n_table = world * self.rows_per_part
+            k = chunks if chunks is not None else default_chunks(world, e1 - e0, self.fused)
+            if not self.fused:
+                k = 1
+            k = max(1, min(k, self.rows_per_part))
+            # block rows: a multiple of 64 keeps every chunk's x rows 16-B
+            # aligned and the projection's row tiles whole
+            b = (self.rows_per_part + k - 1) // k
+            b = (b + 63) // 64 * 64
+            self.layout = TableLayout(kind, world, k, b, slices, width, s_off)
         else:
-            col = col.clone()
-            n_table = csr.num_nodes
-        lrp = (rp[self.r0:self.r1 + 1] - e0).to(torch.int32).contiguous()
-        self.local = LocalCSR(lrp, col.contiguous(), self.n_local, e1 - e0, degree_order(lrp))
-        # allgather: the table rows every rank needs travel in ONE collective
-        # (zero-filled: padding rows are defined).  Where the edge kernel
-        # recomputes s_src from the gathered Wh row (LeakyReLU, f/4 a power of
-        # two) only Wh travels: 256-B, 128-B-aligned rows at H*F = 64 (the packed
-        # [Wh | s_src] row is 288 B and every gather straddles an extra line).
-        # Otherwise one packed buffer [Wh | s_src].  replicate: the default
-        # separate layout (no collective to feed).
-        # Wh-only tables can also be sliced into column planes (layer.wh_slices,
-        # the single-GPU eval forward's layout): one all-gather per plane.
-        hl = self.f // 4
-        self.wh_only = (exchange == "allgather" and self.f % 4 == 0 and hl > 0 and
-                        (hl & (hl - 1)) == 0 and _default_score(layer))
-        self.slices = 1
-        if self.wh_only:
-            from .layer import wh_slices
-            self.slices = wh_slices(self.heads, self.f, self.concat, 0.2,
-                                    csr.num_edges // max(csr.num_nodes, 1))
-        if self.wh_only and self.slices > 1:
-            self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev,
-                                              slices=self.slices)
-        elif self.wh_only:
-            self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev, wh_only=True)
+            b = (csr.num_nodes + 63) // 64 * 64
+            self.layout = TableLayout(kind, 1, 1, b, slices, width, s_off)
+        lay = self.layout
+        self.chunks = lay.chunks
+        self.slices = slices
+        self.wh_only = kind != "packed"
+        self.local = self._local_csr(csr, e0, e1, dev)
+        self.table = torch.zeros(lay.numel, dtype=torch.float32, device=dev)
+        n_sd = csr.num_nodes if exchange == "replicate" else self.n_local
+        self.s_dst = torch.empty(max(n_sd, 1), heads, dtype=torch.float32, device=dev)
+        blk = lay.block_rows if exchange == "allgather" else csr.num_nodes
+        self.s_scratch = (torch.empty(max(blk, 1), heads, dtype=torch.float32, device=dev)
+                          if kind == "wh" else None)
+        width_out = hf if self.concat else f
+        self.out = torch.empty(self.n_local, width_out, dtype=torch.float32, device=dev)
+        if self.chunks > 1:
+            self.st_acc = torch.empty(max(self.n_local, 1), (hf + 3) // 4 * 4,
+                                      dtype=torch.float32, device=dev)
+            self.st_ml = torch.empty(max(self.n_local, 1), 2 * heads, dtype=torch.float32,
+                                     device=dev)
         else:
-            self.table = self.ops.alloc_table(n_table, self.heads, self.f, dev,
-                                              packed=(exchange == "allgather"))
-        self.s_dst_full = torch.empty(csr.num_nodes if exchange == "replicate" else self.n_local,
-                                      self.heads, dtype=torch.float32, device=dev)
-        width = self.heads * self.f if self.concat else self.f
-        self.out = torch.empty(self.n_local, width, dtype=torch.float32, device=dev)
+            self.st_acc = self.st_ml = None
+        if exchanger is None:
+            exchanger = CollectiveExchange(group) if (exchange == "allgather" and world > 1) \
+                else NoExchange()
+        self.exchanger = exchanger
 
-    # -- the three phases of a step (split so compute can be graph-captured) --
-    def phase_project(self, x):
+    def _local_csr(self, csr, e0: int, e1: int, dev) -> LocalCSR:
+        """This rank's rows with source ids remapped to table rows, sorted
+        within each row by table row, and the per-pass segment bounds."""
+        lay = self.layout
+        rp = csr.rowptr
+        lrp = (rp[self.r0:self.r1 + 1] - e0).to(torch.int64)
+        col = csr.col[e0:e1].to(torch.int64)
         if self.exchange == "allgather":
-            m = self.rows_per_part
-            slot = self.table.rows(self.rank * m, self.rank * m + self.n_local)
-            self.ops.project(x, self.pp, self.heads, self.f, slot, self.s_dst_full)
+            b = torch.tensor(self.bounds, dtype=torch.int64, device=dev)
+            owner = torch.searchsorted(b[1:], col, right=True)
+            trow = lay.row_of(owner, col - b[owner])
         else:
-            self.ops.project(x, self.pp, self.heads, self.f, self.table, self.s_dst_full)
+            trow = lay.row_of(torch.zeros_like(col), col)
+        deg = lrp[1:] - lrp[:-1]
+        row_id = torch.repeat_interleave(torch.arange(self.n_local, device=dev), deg)
+        # sources ascending by table row inside each row: each pass's sources
+        # are one contiguous segment, and concurrently scheduled rows sweep the
+        # table in step (the L2 locality of the single-GPU CSR)
+        key = row_id * lay.table_rows + trow
+        key, _ = torch.sort(key)
+        trow = key - row_id * lay.table_rows
+        seg = torch.empty(lay.chunks + 1, self.n_local, dtype=torch.int32, device=dev)
+        seg[0] = lrp[:-1].to(torch.int32)
+        if lay.chunks > 1:
+            ch = lay.chunk_of_row(trow)
+            cnt = torch.zeros(self.n_local * lay.chunks, dtype=torch.int64, device=dev)
+            cnt.index_add_(0, row_id * lay.chunks + ch, torch.ones_like(ch))
+            cum = lrp[:-1].unsqueeze(1) + cnt.view(self.n_local, lay.chunks).cumsum(1)
+            seg[1:] = cum.t().to(torch.int32)
+        else:
+            seg[1] = lrp[1:].to(torch.int32)
+        lrp32 = lrp.to(torch.int32).contiguous()
+        return LocalCSR(lrp32, trow.to(torch.int32).contiguous(), self.n_local, e1 - e0,
+                        degree_order(lrp32), seg.contiguous())
+
+    # -- the pieces of a step ------------------------------------------------
+    def local_x(self, x_full):
+        """This rank's input rows (allgather) or all of x (replicate).  A fresh
+        copy: a row view of x starts off a 16-B boundary whenever r0 * Fin is
+        not a multiple of 4, and the projection kernels load x in float4s."""
+        return x_full[self.r0:self.r1].clone() if self.exchange == "allgather" else x_full
+
+    def project_chunk(self, xl, c: int) -> None:
+        lay = self.layout
+        if self.exchange == "replicate":
+            self.ops.project_rows(xl, self.pp, self.heads, self.f, lay, self.table, 0,
+                                  self.s_dst, self.s_scratch)
+            return
+        lo = c * lay.block_rows
+        hi = min(lo + lay.block_rows, self.n_local)
+        if hi <= lo:
+            return
+        self.ops.project_rows(xl[lo:hi], self.pp, self.heads, self.f, lay, self.table,
+                              lay.block_offset(c, self.rank), self.s_dst[lo:hi], self.s_scratch)
+
+    def exchange_start(self, c: int):
+        if self.exchange != "allgather" or self.world == 1:
+            return None
+        lo, hi = self.layout.chunk_range(c)
+        off = self.layout.block_offset(c, self.rank)
+        return self.exchanger.start(self.table[lo:hi],
+                                    self.table[off:off + self.layout.block_floats])
+
+    def edge_pass(self, c: int):
+        k = self.chunks
+        flags = (_lib.GAT_SEG_LOAD if c > 0 else 0) | (_lib.GAT_SEG_STORE if c < k - 1 else 0)
+        s_dst = self.s_dst[self.r0:self.r1] if self.exchange == "replicate" else self.s_dst
+        return self.ops.edge_pass(self.local, c, self.layout, self.table, s_dst, self.pp,
+                                  self.bias, self.heads, self.f, self.concat, self.act,
+                                  self.param, self.out, self.st_acc, self.st_ml, flags)
+
+    def forward(self, xl):
+        """One step: x = this rank's rows (allgather) or all rows (replicate)."""
+        if self.exchange == "replicate":
+            self.project_chunk(xl, 0)
+            return self.edge_pass(0)
+        handles = []
+        for c in range(self.chunks):
+            self.project_chunk(xl, c)
+            handles.append(self.exchange_start(c))
+        for c in range(self.chunks):
+            self.exchanger.wait(handles[c])
+            self.edge_pass(c)
+        return self.out
+
+    # split phases, for timing the collective and the compute alone
+    def phase_project(self, xl):
+        for c in range(self.chunks):
+            self.project_chunk(xl, c)
 
     def phase_exchange(self):
-        if self.exchange == "allgather" and self.world > 1:
-            m = self.rows_per_part
-            # one in-place all-gather per column plane (a single one for the
-            # row-major table)
-            planes = [self.table.buf[g] for g in range(self.slices)] if self.slices > 1 \
-                else [self.table.buf]
-            for buf in planes:
-                dist.all_gather_into_tensor(buf, buf[self.rank * m:(self.rank + 1) * m],
-                                            group=self.group)
+        hs = [self.exchange_start(c) for c in range(self.chunks)]
+        for h in hs:
+            self.exchanger.wait(h)
 
     def phase_edges(self):
-        s_dst = self.s_dst_full if self.exchange == "allgather" else \
-            self.s_dst_full[self.r0:self.r1]
-        return self.ops.edge_aggregate(self.local, self.table, s_dst, self.heads, self.f,
-                                       self.concat, self.bias, 0.2, self.out, pp=self.pp)
+        for c in range(self.chunks):
+            self.edge_pass(c)
+        return self.out
 
-    def forward(self, x):
-        """x: this rank's rows [n_local, Fin] (allgather) or all rows (replicate)."""
-        self.phase_project(x)
-        self.phase_exchange()
-        return self.phase_edges()
 
-    def local_x(self, x_full):
-        # a fresh copy: a row view of x can start off a 16-B boundary, which the
-        # whole-K projection (the one that writes the sliced table) needs
-        return x_full[self.r0:self.r1].clone() if self.exchange == "allgather" else x_full
+def emulate(layer, csr, x, world: int, exchange: str = "allgather",
+            chunks: Optional[int] = None) -> torch.Tensor:
+    """P ranks in ONE process on one device: every rank's projection, the
+    all-gather emulated by block copies, every rank's edge passes; returns the
+    concatenated output [N, width].  Runs the real kernels on the real
+    per-rank tables, segments and state buffers."""
+    ranks = [ShardedGAT(layer, csr, world, r, exchange=exchange, chunks=chunks,
+                        exchanger=NoExchange()) for r in range(world)]
+    xs = [sh.local_x(x) for sh in ranks]
+    for sh, xl in zip(ranks, xs):
+        sh.phase_project(xl)
+    if exchange == "allgather" and world > 1:
+        lay = ranks[0].layout
+        for c in range(lay.chunks):
+            for src in ranks:
+                off = lay.block_offset(c, src.rank)
+                blk = src.table[off:off + lay.block_floats]
+                for dst in ranks:
+                    if dst is not src:
+                        dst.table[off:off + lay.block_floats].copy_(blk)
+    outs = [sh.phase_edges() for sh in ranks]
+    return torch.cat(outs)
 
 
 def gather_output(local_out: torch.Tensor, bounds: List[int], group=None) -> torch.Tensor:
-    """Concatenate the sharded outputs (for checks only; not part of a step)."""
+    """Concatenate the sharded outputs on every rank (checks only; not part of
+    a step).  Staged through host memory, so any group backend works."""
     world = len(bounds) - 1
     m = max(bounds[k + 1] - bounds[k] for k in range(world))
-    pad = torch.zeros(m, local_out.size(1), dtype=local_out.dtype, device=local_out.device)
-    pad[:local_out.size(0)] = local_out
-    allp = torch.empty(world * m, local_out.size(1), dtype=local_out.dtype,
-                       device=local_out.device)
+    pad = torch.zeros(m, local_out.size(1), dtype=local_out.dtype)
+    pad[:local_out.size(0)] = local_out.cpu()
+    allp = torch.empty(world * m, local_out.size(1), dtype=local_out.dtype)
     dist.all_gather_into_tensor(allp, pad, group=group)
     return torch.cat([allp[k * m:k * m + bounds[k + 1] - bounds[k]] for k in range(world)])
 
@@ -216,7 +472,7 @@ def gather_output(local_out: torch.Tensor, bounds: List[int], group=None) -> tor
 # ---------------------------------------------------------------------------
 # bench.py --gpus N (torchrun, one process per GPU, RCCL)
 # ---------------------------------------------------------------------------
-def _time_steps(step, warmup: int, steps: int, dev) -> float:
+def _time_steps(step, warmup: int, steps: int) -> float:
     """W untimed steps, then K steps bracketed by barrier + synchronize on both
     sides; returns the MAX over ranks of the K-step wall time (seconds).  Each
     rank's clock runs from just after the opening barrier to its own final
@@ -233,85 +489,149 @@ def _time_steps(step, warmup: int, steps: int, dev) -> float:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     dist.barrier()
-    # the default group is gloo (bench_distributed): a host tensor
-    t = torch.tensor([elapsed], dtype=torch.float64)
+    t = torch.tensor([elapsed], dtype=torch.float64)  # default group: gloo, on the host
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def _strong_probe(w, layer, dev, world, rank, exchange, steps, warmup, use_graph, group=None):
-    """ONE shared graph of the workload's shape, node-range partitioned across
-    the ranks: per step, project own rows -> RCCL all-gather of
-    the packed [Wh | s_src] table (exchange="allgather") or full projection on
-    every rank (exchange="replicate") -> local edge kernel."""
-    from .graph import get_csr
+def _event_ms(fn, iters: int) -> float:
+    """Mean GPU time of fn over iters, HIP events on the current stream."""
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    e0.record(s)
+    for _ in range(iters):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def _make_layer(w, dev):
+    from .layer import GraphAttentionLayer
+    torch.manual_seed(0)
+    return GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
+                               concat=w.concat).to(dev).eval()
+
+
+def _sharded_workload(w, dev, world: int, rank: int, exchanger, args, chunk_choices) -> Dict:
+    """ONE shared graph of workload w, node-range partitioned over the ranks
+    (SURVEY.md §8e): per step, project own rows -> chunked RCCL all-gather ->
+    edge passes.  Also on rank 0: the same layer forward on the whole graph on
+    one GPU (the 1-GPU reference for this workload) and a check that the
+    gathered sharded output equals it."""
+    from .graph import build_csr
     from .synthetic import make_inputs
 
     x, ei = make_inputs(w, dev)  # same seeds on every rank -> the same graph
-    csr = get_csr(ei, x.size(0))
-    del ei
-    sh = ShardedGAT(layer, csr, world, rank, exchange=exchange, group=group)
-    xl = sh.local_x(x)
-    launch = "eager"
-    g_proj = g_edge = None
-    for _ in range(3):
+    csr = build_csr(ei, x.size(0))
+    layer = _make_layer(w, dev)
+    res = {"workload": w.name, "N": x.size(0), "E_prime": csr.num_edges,
+           "Fin": w.in_channels, "H": w.heads, "F": w.out_channels}
+    ref = None
+    with torch.no_grad():
+        if rank == 0:  # the single-GPU forward of the same workload (others wait)
+            from .layer import gat_forward
+            pp = layer.packed()
+            bias = layer.bias.detach()
+
+            def one():
+                return gat_forward(x, csr, pp, bias, w.heads, w.out_channels, w.concat,
+                                   layer.negative_slope)
+            for _ in range(3):
+                ref = one()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                one()
+            torch.cuda.synchronize()
+            ms1 = (time.perf_counter() - t0) * 1e3 / args.steps
+            ref = one().cpu()
+            res["one_gpu"] = {"value": csr.num_edges / (ms1 * 1e-3), "ms_per_step": ms1,
+                              "what": "the same layer forward on the whole graph on rank 0's "
+                                      "GPU alone (bench.py's single-GPU path)"}
+        dist.barrier()
+        del ei
+        # chunk count: try each candidate for a few steps, keep the fastest
+        tried = {}
+        best = None
+        for k in chunk_choices:
+            sh = ShardedGAT(layer, csr, world, rank, chunks=k, exchanger=exchanger)
+            if sh.chunks != k and k != 1:
+                continue
+            xl = sh.local_x(x)
+            t = _time_steps(lambda: sh.forward(xl), 2, 5)
+            tried[k] = t * 1e3 / 5
+            if best is None or tried[k] < tried[best[0]]:
+                best = (k, sh, xl)
+            else:
+                del sh
+        k, sh, xl = best
+        t = _time_steps(lambda: sh.forward(xl), args.warmup, args.steps)
+        ms = t * 1e3 / args.steps
+        # the pieces alone (max over ranks): collective, projection, edge passes
+        t_ex = _time_steps(sh.phase_exchange, 2, args.steps) * 1e3 / args.steps \
+            if world > 1 else 0.0
+        proj_ms = _event_ms(lambda: sh.phase_project(xl), args.steps)
+        edge_ms = _event_ms(sh.phase_edges, args.steps)
+        # check: gathered sharded output == the single-GPU forward
         sh.forward(xl)
-    torch.cuda.synchronize()
-    if use_graph:
-        try:  # capture the compute phases; the collective runs between them
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                sh.phase_project(xl)
-                sh.phase_edges()
-            torch.cuda.current_stream().wait_stream(s)
-            g_proj, g_edge = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_proj):
-                sh.phase_project(xl)
-            with torch.cuda.graph(g_edge):
-                sh.phase_edges()
-            launch = "hipGraph(project) + collective + hipGraph(edges)"
-        except Exception as exc:  # capture unsupported -> eager
-            g_proj = g_edge = None
-            launch = f"eager (graph capture failed: {type(exc).__name__})"
+        full = gather_output(sh.out, sh.bounds)
+    res.update({
+        "value": csr.num_edges / (ms * 1e-3), "unit": "edges/s", "ms_per_step": ms,
+        "chunks": k, "chunk_trials_ms": tried, "collective_ms": t_ex,
+        "rank0_project_ms": proj_ms, "rank0_edge_passes_ms": edge_ms,
+        "rows_per_rank": sh.rows_per_part, "table_bytes": int(sh.table.numel() * 4),
+        "table_layout": sh.layout.kind, "planes": sh.slices,
+        "rank0_local_edges": sh.local.num_edges,
+    })
+    if rank == 0:
+        diff = float((full - ref).abs().max())
+        scale = float(ref.abs().max())
+        res["check"] = {"max_abs_diff_vs_one_gpu": diff, "max_abs_ref": scale}
+        if not diff <= 1e-5 + 1e-5 * scale:
+            raise RuntimeError(f"sharded {w.name} output differs from the single-GPU forward: "
+                               f"max |diff| {diff:.3e} (max |ref| {scale:.3e})")
+    del sh, x, csr
+    torch.cuda.empty_cache()
+    return res
 
-    def step():
-        if g_proj is not None:
-            g_proj.replay()
-            sh.phase_exchange()
-            g_edge.replay()
-        else:
-            sh.forward(xl)
 
-    t = _time_steps(step, warmup, steps, dev)
-    ex_ms = None
-    if exchange == "allgather" and world > 1:
-        t_ex = _time_steps(sh.phase_exchange, 3, steps, dev)
-        ex_ms = t_ex * 1e3 / steps
-    ms = t * 1e3 / steps
-    return {"exchange": exchange, "value": csr.num_edges / (ms * 1e-3), "unit": "edges/s",
-            "ms_per_step": ms, "collective_ms": ex_ms, "rows_per_rank": sh.rows_per_part,
-            "table_bytes": int(sh.table.wh.numel() * 4) if exchange == "allgather" else None,
-            "launch": launch}
+def _ppi_blocks_weak(w, dev, world: int, rank: int, args) -> Dict:
+    """Secondary: data-parallel PPI-shape blocks (the real PPI dataset is a set
+    of disjoint graphs): rank k owns one block seeded +1000k, the halo is empty
+    and the step has no collective.  Weak scaling."""
+    from .graph import get_csr
+    from .synthetic import make_inputs
+    layer = _make_layer(w, dev)
+    x, ei = make_inputs(w, dev, x_seed=1 + 1000 * rank, edge_seed=2 + 1000 * rank)
+    csr = get_csr(ei, x.size(0))
+    with torch.no_grad():
+        t = _time_steps(lambda: layer(x, ei), args.warmup, args.steps)
+    e_blk = torch.tensor([csr.num_edges], dtype=torch.float64)
+    dist.all_reduce(e_blk)
+    ms = t * 1e3 / args.steps
+    return {"value": float(e_blk.item()) / (ms * 1e-3), "unit": "edges/s", "ms_per_step": ms,
+            "scaling": "weak",
+            "what": f"{world} disjoint PPI-shape blocks, one per GPU (N={x.size(0)}, "
+                    f"E'={csr.num_edges} each); no collective in the step"}
 
 
 def bench_distributed(args, metric: str):
-    """One process per GPU.  The reported line is WEAK scaling: every rank owns
-    one PPI-shape block of a block-diagonal graph (the real PPI dataset is a set
-    of disjoint graphs), so the node-range partition falls on block boundaries,
-    the halo is empty and the step needs no collective; value = world x E'
-    per block / max-over-ranks step time.  The same run also measures the
-    STRONG-scaling north-star path on one shared graph (RCCL all-gather of the
-    packed table, and the replicate alternative) and reports it under
-    "strong_scaling"."""
-    from .layer import GraphAttentionLayer
-    from .synthetic import WORKLOADS, make_inputs
-    from .graph import get_csr
+    """One process per GPU (torchrun).  The reported line is the north-star
+    path on ONE shared Reddit-scale graph (BASELINE.json
+    configs[4]): node-range partition, chunked RCCL all-gather of the node
+    table inside the timed step, edge passes overlapped with it.  Strong
+    scaling: total work is fixed as N grows.  ogbn-arxiv scale (configs[3])
+    runs the same way under "workloads"; the data-parallel PPI-block run is a
+    secondary field."""
+    from .synthetic import WORKLOADS
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if os.environ.get("GAT_BENCH_SHARE_GPU0"):  # testing on a one-GPU box: every rank on cuda:0
+    share = bool(os.environ.get("GAT_BENCH_SHARE_GPU0"))  # rehearsal: every rank on cuda:0
+    if share:
         local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -320,110 +640,48 @@ def bench_distributed(args, metric: str):
     sys.stdout.flush()
     saved_stdout = os.dup(1)
     os.dup2(2, 1)
-    # The weak-scaling step has no data-path collective, so the default group is
-    # gloo (barriers and the max-over-ranks reduction on the host): no RCCL
-    # proxy threads compete with the launch thread while it is timed.  The RCCL
-    # group is created afterwards, for the strong-scaling probe's all-gather.
-    # single node, rendezvous on 127.0.0.1: keep gloo on loopback rather than on
-    # whatever interface the (possibly unresolvable) hostname maps to
+    # default group gloo: barriers and the max-over-ranks reduction on the host;
+    # the table all-gather runs on an RCCL group (nccl backend = RCCL on ROCm)
     os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     dist.init_process_group("gloo")
-
-    w = WORKLOADS[args.workload]
-    torch.manual_seed(0)
-    layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
-                                concat=w.concat).to(dev).eval()
-
-    def layer_for(pw):
-        if pw is w:
-            return layer
-        torch.manual_seed(0)
-        return GraphAttentionLayer(pw.in_channels, pw.out_channels, num_heads=pw.heads,
-                                   concat=pw.concat).to(dev).eval()
-    # this rank's block: seeds offset by rank (rank 0's block is the 1-GPU graph)
-    x, ei = make_inputs(w, dev, x_seed=1 + 1000 * rank, edge_seed=2 + 1000 * rank)
-    csr = get_csr(ei, x.size(0))
-    with torch.no_grad():
-        for _ in range(3):
-            layer(x, ei)
-        torch.cuda.synchronize()
-        step, launch = (lambda: layer(x, ei)), "eager"
-        if args.graph:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                layer(x, ei)
-            torch.cuda.current_stream().wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                layer(x, ei)
-            step, launch = g.replay, "hipGraph"
-        t = _time_steps(step, args.warmup, args.steps, dev)
-        ms = t * 1e3 / args.steps
-        e_blk = torch.tensor([csr.num_edges], dtype=torch.float64)
-        dist.all_reduce(e_blk)
-        total_edges = float(e_blk.item())
-
-        # edge kernel alone on this rank's block (roofline), in the layer's table
-        # layout, HIP events on its stream
-        from bench import time_edge_kernel
-        edge_ms, slices = time_edge_kernel(layer, x, csr, args.edge_iters)
-        n_block = x.size(0)
-        del x, ei
-
-        strong = []
-        if not getattr(args, "no_strong_probe", False):
-            # evidence only (the reported value is the weak-scaling line): a failure
-            # here is recorded in the JSON instead of costing the line
-            try:
-                rccl = dist.new_group(backend="nccl")
-            except Exception as exc:  # noqa: BLE001
-                rccl = None
-                strong.append({"error": f"RCCL group: {type(exc).__name__}: {exc}"[:300]})
-            if rccl is not None:
-                probes = [(w, "allgather"), (w, "replicate")]
-                if (world > 1 or os.environ.get("GAT_BENCH_PROBE_REDDIT")) and w.name == "ppi":
-                    # the shape the all-gather is designed for: edge work
-                    # shrinks as 1/N while the exchanged table is 67 MB; its 1-GPU
-                    # reference is `bench.py --workload reddit`
-                    probes.append((WORKLOADS["reddit"], "allgather"))
-                for pw, ex in probes:
-                    try:
-                        r = _strong_probe(pw, layer_for(pw), dev, world, rank, ex,
-                                          max(args.steps // 2, 5), max(args.warmup // 2, 2),
-                                          not args.no_graph, group=rccl)
-                        r["workload"] = pw.name
-                        strong.append(r)
-                    except Exception as exc:  # noqa: BLE001
-                        strong.append({"workload": pw.name, "exchange": ex,
-                                       "error": f"{type(exc).__name__}: {exc}"[:300]})
-                    torch.cuda.empty_cache()
-
-    from bench import HBM_PEAK_GBS, edge_kernel_bytes, edge_kernel_name, load_traffic  # noqa: E402
-    alg = edge_kernel_bytes(n_block, csr.num_edges, w.heads, w.out_channels, w.concat)
-    ach = alg / (edge_ms * 1e-3) / 1e9
+    if world > 1 and not share:
+        exchanger = CollectiveExchange(dist.new_group(backend="nccl"))
+        xname = "RCCL all_gather_into_tensor (in place, async, one per chunk)"
+    elif world > 1:
+        exchanger = HostStagedExchange(None)
+        xname = "gloo all-gather staged through host memory (one-GPU rehearsal)"
+    else:
+        exchanger = NoExchange()
+        xname = "none (one rank)"
+    names = [s for s in getattr(args, "dist_workloads", "reddit,arxiv").split(",") if s]
+    chunk_choices = [1, 2, 4] if world > 1 else [1]
+    work = {}
+    for nm in names:
+        work[nm] = _sharded_workload(WORKLOADS[nm], dev, world, rank, exchanger, args,
+                                     chunk_choices)
+    weak = None
+    if not getattr(args, "no_weak", False):
+        weak = _ppi_blocks_weak(WORKLOADS["ppi"], dev, world, rank, args)
     res = None
     if rank == 0:
+        head = work[names[0]]
+        w = WORKLOADS[names[0]]
         res = {
-            "metric": metric, "value": total_edges / (ms * 1e-3), "unit": "edges/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded uniform PPI-shape blocks, one per GPU; reference-order "
-                    "random init)",
-            "config": {"workload": f"{w.name} x {world}: block-diagonal graph, {world} PPI-shape "
-                                   f"blocks of N={n_block} E'={csr.num_edges} Fin={w.in_channels} "
-                                   f"H={w.heads} F={w.out_channels} concat={w.concat}",
-                       "parallelism": f"node-range partition x{world} on block boundaries "
-                                      "(empty halo: no collective in the step)",
-                       "launch": launch},
-            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": load_traffic(args.workload),
-                         "kernel": edge_kernel_name(slices) + " (rank 0 block)",
-                         "kernel_ms": edge_ms,
-                         "algorithmic_bytes_per_launch": alg},
-            "strong_scaling": {"graph": "one graph of the named workload's shape shared by "
-                                        f"{world} ranks, node-range partitioned",
-                               "runs": strong},
+            "metric": metric, "value": head["value"], "unit": "edges/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded uniform graph of the named shape; reference-order random "
+                    "init)",
+            "config": {"workload": f"{w.name}: N={head['N']} E'={head['E_prime']} "
+                                   f"Fin={w.in_channels} H={w.heads} F={w.out_channels} "
+                                   f"concat={w.concat}, one graph shared by {world} GPUs",
+                       "parallelism": f"node-range partition x{world} (edge-balanced), node "
+                                      f"table all-gathered in {head['chunks']} chunk(s) "
+                                      "overlapped with the edge passes",
+                       "exchange": xname, "launch": "eager"},
+            "one_gpu_same_workload": head.get("one_gpu"),
+            "workloads": work,
+            "ppi_blocks_data_parallel": weak,
         }
     dist.barrier()
     dist.destroy_process_group()

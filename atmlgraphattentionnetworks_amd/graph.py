@@ -3,8 +3,9 @@
 Replaces ``torch_geometric.utils.add_self_loops`` (``GAT.py:38``) and the
 grouping of edges by target that PyG's ``propagate`` / ``softmax`` /
 ``aggregate`` perform on every call (``GAT.py:53,60``).  The CSR is built on
-the GPU by ``gat_csr_build`` (stable radix sort by target, loop appended last
-in each row) and cached per ``edge_index`` tensor, because every caller runs
+the GPU by ``gat_csr_build`` (one stable radix sort of (target, source) keys
+over the input edges plus the N self-loops: rows grouped by target, sources
+ascending within a row) and cached per ``edge_index`` tensor, because every caller runs
 the layer several times on one graph (``GATNet.py:79,85``: two layers per
 forward; the ``run_*.py`` loops: every epoch).
 """
@@ -16,7 +17,25 @@ from typing import NamedTuple, Optional
 
 import torch
 
-from . import _lib
+from . import _lib, tuning
+
+
+class HubPlan(NamedTuple):
+    """Degree-skew schedule (split hub rows, (m, l, acc) merge).
+
+    Rows with more than 2 * seg_len in-edges ("hubs") are cut into segments
+    of seg_len edges that run as separate lane groups of the edge kernel,
+    scheduled ahead of the whole rows; gat_edge_merge then combines each
+    hub's segment states.  Without this, one 100k-edge row walks serially on
+    one lane group and outlasts the rest of the kernel many times over."""
+    n_hub: int
+    n_vrows: int  # segments of all hubs = the first n_vrows schedule positions
+    seg_len: int
+    hub_rows: torch.Tensor  # int32 [n_hub]
+    hub_vptr: torch.Tensor  # int32 [n_hub + 1]: hub k's segments
+    sched_row: torch.Tensor  # int32 [n_vrows + N - n_hub]: target row per position
+    sched_b: torch.Tensor  # int32: CSR range of each position
+    sched_e: torch.Tensor
 
 
 class CSRGraph(NamedTuple):
@@ -25,6 +44,7 @@ class CSRGraph(NamedTuple):
     num_nodes: int
     num_edges: int  # E + N (edges after add_self_loops)
     order: Optional[torch.Tensor] = None  # int32 [N], rows by descending in-degree
+    hubs: Optional[HubPlan] = None  # split schedule for rows far above the average
 
 
 def _check_edge_index(edge_index: torch.Tensor, device: torch.device) -> torch.Tensor:
@@ -39,11 +59,14 @@ def _check_edge_index(edge_index: torch.Tensor, device: torch.device) -> torch.T
     return edge_index.to(torch.int64).contiguous()
 
 
-def build_csr(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
-    """Build the CSR-by-target (with appended self-loops) on ``edge_index``'s GPU."""
+def build_csr(edge_index: torch.Tensor, num_nodes: int,
+              device: Optional[torch.device] = None) -> CSRGraph:
+    """Build the CSR-by-target (with the self-loops added) on ``edge_index``'s
+    GPU.  ``device``: the device of the node features; an ``edge_index`` on
+    another device raises, as the reference's ``index_select`` would."""
     if edge_index.device.type != "cuda":
         raise RuntimeError("build_csr needs a ROCm device tensor; there is no CPU path")
-    ei = _check_edge_index(edge_index, edge_index.device)
+    ei = _check_edge_index(edge_index, edge_index.device if device is None else device)
     lib = _lib.load()
     E = ei.size(1)
     dev = ei.device
@@ -61,7 +84,54 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
     if int(flag.item()) != 0:
         # PyG's index_select raises on the same input (GAT.py:53 -> __lift__)
         raise ValueError(f"edge_index contains node ids outside [0, {num_nodes})")
-    return CSRGraph(rowptr, col, num_nodes, E + num_nodes, order)
+    return CSRGraph(rowptr, col, num_nodes, E + num_nodes, order,
+                    hub_plan(rowptr, order, E + num_nodes))
+
+
+def hub_segment_len(num_edges: int) -> int:
+    """Edges per hub segment: a power of two in [256, 2048], ~E'/50000 (a
+    segment should take a small fraction of the whole edge kernel: PPI and
+    arxiv scale 256, Reddit scale 2048).  GAT_HUB_SEG overrides."""
+    env = tuning.get("GAT_HUB_SEG")
+    if env is not None:
+        return max(16, int(env))
+    s = 256
+    while s < 2048 and 2 * s <= num_edges // 50000:
+        s *= 2
+    return s
+
+
+def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
+             seg_len: Optional[int] = None) -> Optional[HubPlan]:
+    """The split schedule for rows with more than 2 * seg_len in-edges, or
+    None when there are none (every uniform BASELINE graph).  ``order`` is
+    the degree-descending row order, so the hubs are its first rows.
+    GAT_HUB_SPLIT=0 disables splitting."""
+    if tuning.get("GAT_HUB_SPLIT") == "0" or rowptr.numel() <= 1:
+        return None
+    seg = seg_len or hub_segment_len(num_edges)
+    deg = (rowptr[1:] - rowptr[:-1]).to(torch.int64)
+    n_hub = int((deg > 2 * seg).sum())
+    if n_hub == 0:
+        return None
+    o = order.to(torch.int64)
+    hub_rows = o[:n_hub]
+    hdeg = deg[hub_rows]
+    nseg = (hdeg + seg - 1) // seg
+    vptr = torch.zeros(n_hub + 1, dtype=torch.int64, device=rowptr.device)
+    vptr[1:] = nseg.cumsum(0)
+    n_v = int(vptr[-1])
+    vhub = torch.repeat_interleave(torch.arange(n_hub, device=rowptr.device), nseg)
+    k = torch.arange(n_v, device=rowptr.device) - vptr[vhub]
+    rp = rowptr.to(torch.int64)
+    vb = rp[hub_rows][vhub] + k * seg
+    ve = torch.minimum(vb + seg, rp[hub_rows + 1][vhub])
+    rest = o[n_hub:]
+    i32 = torch.int32
+    return HubPlan(n_hub, n_v, seg, hub_rows.to(i32).contiguous(), vptr.to(i32).contiguous(),
+                   torch.cat([hub_rows[vhub], rest]).to(i32).contiguous(),
+                   torch.cat([vb, rp[rest]]).to(i32).contiguous(),
+                   torch.cat([ve, rp[rest + 1]]).to(i32).contiguous())
 
 
 class _CSRCache:
@@ -71,14 +141,18 @@ class _CSRCache:
         self.capacity = capacity
         self._entries = collections.OrderedDict()
 
-    def get(self, edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
+    def get(self, edge_index: torch.Tensor, num_nodes: int,
+            device: Optional[torch.device] = None) -> CSRGraph:
+        if device is not None and isinstance(edge_index, torch.Tensor) and \
+                edge_index.device != device:
+            raise ValueError(f"edge_index is on {edge_index.device} but x is on {device}")
         key = (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape),
                edge_index.dtype, num_nodes, edge_index.device)
         hit = self._entries.get(key)
         if hit is not None and hit[0]() is edge_index:
             self._entries.move_to_end(key)
             return hit[1]
-        csr = build_csr(edge_index, num_nodes)
+        csr = build_csr(edge_index, num_nodes, device)
         self._entries[key] = (weakref.ref(edge_index), csr)
         while len(self._entries) > self.capacity:
             self._entries.popitem(last=False)
@@ -91,8 +165,9 @@ class _CSRCache:
 csr_cache = _CSRCache()
 
 
-def get_csr(edge_index: torch.Tensor, num_nodes: int) -> CSRGraph:
-    return csr_cache.get(edge_index, num_nodes)
+def get_csr(edge_index: torch.Tensor, num_nodes: int,
+            device: Optional[torch.device] = None) -> CSRGraph:
+    return csr_cache.get(edge_index, num_nodes, device)
 
 
 class CSCGraph(NamedTuple):

@@ -21,17 +21,16 @@ No PyG import, no CPU path: a CPU tensor or a missing library raises.
 from __future__ import annotations
 
 import itertools
-import os
 import weakref
 from typing import NamedTuple, Optional, Tuple
 
 import torch
 
-from . import _lib
+from . import _lib, tuning
 from .graph import CSRGraph, get_csr
 
 __all__ = ["GraphAttentionLayer", "GraphAttentionLayerActivationTest", "score_activation_code",
-           "PackedParams", "pack_params", "gat_forward", "wh_slices", "NodeTable",
+           "PackedParams", "pack_params", "gat_forward", "ForwardPlan", "wh_slices", "NodeTable",
            "alloc_table", "project", "edge_aggregate"]
 
 
@@ -200,7 +199,7 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
     if out is None:
         out = torch.empty(rows, width, dtype=torch.float32, device=table.wh.device)
     order = getattr(csr, "order", None)
-    if order is not None and os.environ.get("GAT_EDGE_ORDER") == "natural":  # A/B knob
+    if order is not None and tuning.get("GAT_EDGE_ORDER") == "natural":  # A/B knob
         order = None
     hint = csr.num_edges // max(csr.num_nodes, 1)
     if table.slices > 1:
@@ -239,7 +238,7 @@ def wh_slices(heads: int, f: int, concat: bool, negative_slope: float,
     (56.6 -> 61.8 us: each plane re-reads the row's indices and bookkeeping).
     ``GAT_WH_SLICES`` (A/B knob) overrides the default."""
     hf = heads * f
-    env = os.environ.get("GAT_WH_SLICES")
+    env = tuning.get("GAT_WH_SLICES")
     if env is not None:
         s = int(env)
     elif hf % _PLANE_COLS == 0 and edges_per_row >= _MIN_SLICED_EPR:
@@ -259,9 +258,128 @@ _PLANE_COLS = 32        # 128-byte plane rows
 _MIN_SLICED_EPR = 16    # average in-edges per row below which row-major wins
 
 
+def fused_score_ok(heads: int, f: int, negative_slope: float) -> bool:
+    """Shapes the fused-score edge kernels take (the source score recomputed
+    from the gathered Wh row): LeakyReLU slope in [0, 1], f % 4 == 0 and f/4 a
+    power of two."""
+    hl = f // 4
+    return 0.0 <= negative_slope <= 1.0 and f % 4 == 0 and hl > 0 and (hl & (hl - 1)) == 0
+
+
+def _edge_hubs(lib, csr: CSRGraph, wh_ptr: int, ld_wh: int, n_table: int, slices: int,
+               pp: PackedParams, p_sd: int, heads: int, f: int, concat: bool,
+               negative_slope: float, bias: torch.Tensor, out: torch.Tensor, stream: int) -> None:
+    """Edge kernel with the hub rows split (graph.HubPlan): one launch over the
+    hub segments (state stored) and the whole rows (output written), then
+    gat_edge_merge for the hubs."""
+    hubs = csr.hubs
+    hf4 = (heads * f + 3) // 4 * 4
+    nv = hubs.n_vrows
+    st = torch.empty(nv * (hf4 + 2 * heads), dtype=torch.float32, device=out.device)
+    p_acc = st.data_ptr()
+    p_ml = p_acc + 4 * nv * hf4
+    n_pos = hubs.sched_row.numel()
+    hint = csr.num_edges // max(csr.num_nodes, 1)
+    rc = lib.gat_edge_aggregate_seg(
+        hubs.sched_b.data_ptr(), hubs.sched_e.data_ptr(), 1, csr.col.data_ptr(),
+        hubs.sched_row.data_ptr(), 0, n_pos, wh_ptr, ld_wh, n_table, slices,
+        pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, heads, f, int(concat),
+        float(negative_slope), p_acc, p_ml, 0, nv, bias.data_ptr(), out.data_ptr(), hint, stream)
+    if rc:
+        _lib.check(rc, "gat_edge_aggregate_seg (hub split)")
+    rc = lib.gat_edge_merge(hubs.hub_rows.data_ptr(), hubs.hub_vptr.data_ptr(), hubs.n_hub,
+                            p_acc, p_ml, heads, f, int(concat), bias.data_ptr(), out.data_ptr(),
+                            0, 0, stream)
+    if rc:
+        _lib.check(rc, "gat_edge_merge")
+
+
+class ForwardPlan:
+    """The eval forward's launch plan for one (x, graph, layer shape): the
+    workspace (Wh | s_src | s_dst), the table layout and the edge path.
+    ``gat_forward`` builds one per call; ``bench.py`` keeps one to time the
+    two phases of exactly the path the layer runs."""
+
+    __slots__ = ("n", "fin", "heads", "f", "hf", "hfp", "concat", "slope", "slices", "split",
+                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint")
+
+    def __init__(self, x: torch.Tensor, csr: CSRGraph, heads: int, f: int, concat: bool,
+                 negative_slope: float):
+        n, fin = x.shape
+        self.n, self.fin, self.heads, self.f, self.concat = n, fin, heads, f, concat
+        self.slope = float(negative_slope)
+        self.hf = heads * f
+        self.hfp = (self.hf + 3) // 4 * 4
+        self.ws = torch.empty(n * (self.hfp + 2 * heads), dtype=torch.float32, device=x.device)
+        self.p_wh = self.ws.data_ptr()
+        self.p_ss = self.p_wh + 4 * n * self.hfp
+        self.p_sd = self.p_ss + 4 * n * heads
+        self.dev = x.device.index
+        self.hint = csr.num_edges // max(n, 1)
+        self.slices = wh_slices(heads, f, concat, negative_slope, self.hint)
+        self.split = csr.hubs is not None and fused_score_ok(heads, f, negative_slope)
+
+    def project(self, lib, x: torch.Tensor, pp: PackedParams) -> None:
+        """gat_project(_sliced) into the workspace (GAT.py:42-52)."""
+        n, fin, heads, f = self.n, self.fin, self.heads, self.f
+        stream = torch._C._cuda_getCurrentRawStream(self.dev)  # the current stream, per call
+        if self.slices > 1:
+            rc = lib.gat_project_sliced(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                                        pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+                                        pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
+                                        self.slices, self.p_wh, n, 0, heads, self.p_sd,
+                                        stream)
+            if rc == 0:
+                return
+            if rc != _lib.GAT_EUNSUPPORTED:
+                _lib.check(rc, "gat_project_sliced")
+            self.slices = 1  # nothing was launched: the row-major table instead
+        rc = lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                             pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
+                             pp.c_dst.data_ptr(), heads, f, self.p_wh, self.hfp, self.p_ss,
+                             heads, self.p_sd, stream)
+        if rc:
+            _lib.check(rc, "gat_project")
+
+    def edge(self, lib, csr: CSRGraph, pp: PackedParams, bias: torch.Tensor,
+             out: torch.Tensor) -> torch.Tensor:
+        """The edge kernel(s) over the table project() wrote (GAT.py:53-67, +bias)."""
+        n, heads, f = self.n, self.heads, self.f
+        stream = torch._C._cuda_getCurrentRawStream(self.dev)
+        if self.split:
+            ld = self.hf // self.slices if self.slices > 1 else self.hfp
+            _edge_hubs(lib, csr, self.p_wh, ld, n, self.slices, pp, self.p_sd, heads, f,
+                       self.concat, self.slope, bias, out, stream)
+            return out
+        p_order = 0 if csr.order is None else csr.order.data_ptr()
+        if self.slices > 1:
+            rc = lib.gat_edge_aggregate_sliced(
+                csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, self.p_wh, n,
+                self.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
+                self.slope, bias.data_ptr(), out.data_ptr(), self.hint, stream)
+            if rc:
+                _lib.check(rc, "gat_edge_aggregate_sliced")
+            return out
+        rc = lib.gat_edge_aggregate(
+            csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, self.p_wh, self.hfp,
+            self.p_ss, heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
+            int(self.concat), self.slope, bias.data_ptr(), out.data_ptr(), 0, self.hint, stream)
+        if rc:
+            _lib.check(rc, "gat_edge_aggregate")
+        return out
+
+    def kernel_name(self) -> str:
+        if self.split:
+            return "gat_edge_aggregate_seg (k_edge_grp, hub rows split) + gat_edge_merge"
+        if self.slices > 1:
+            return f"gat_edge_aggregate_sliced (k_edge_grp, {self.slices} column planes)"
+        return "gat_edge_aggregate (k_edge_grp)"
+
+
 def gat_forward(x: torch.Tensor, csr: CSRGraph, pp: PackedParams, bias: torch.Tensor,
                 heads: int, f: int, concat: bool, negative_slope: float = 0.2) -> torch.Tensor:
-    """Layer forward on prepared inputs: projection + edge kernel (2 launches).
+    """Layer forward on prepared inputs: projection + edge kernel (2 launches;
+    3 when hub rows are split).
 
     Lean host path (it is on the critical path for graphs the size of PPI,
     where the GPU work is ~50 us): one workspace allocation holding
@@ -269,47 +387,10 @@ def gat_forward(x: torch.Tensor, csr: CSRGraph, pp: PackedParams, bias: torch.Te
     ``wh_slices(...) > 1`` Wh is stored as column planes (``gat_amd.h``,
     sliced node table) and the edge kernel runs one plane per workgroup."""
     lib = _lib.load()
-    n, fin = x.shape
-    hf = heads * f
-    hfp = (hf + 3) // 4 * 4
-    dev = x.device
-    ws = torch.empty(n * (hfp + 2 * heads), dtype=torch.float32, device=dev)
-    out = torch.empty(n, hf if concat else f, dtype=torch.float32, device=dev)
-    p_wh = ws.data_ptr()
-    p_ss = p_wh + 4 * n * hfp
-    p_sd = p_ss + 4 * n * heads
-    stream = torch._C._cuda_getCurrentRawStream(dev.index)
-    order = csr.order
-    p_order = 0 if order is None else order.data_ptr()
-    hint = csr.num_edges // max(n, 1)
-    slices = wh_slices(heads, f, concat, negative_slope, hint)
-    if slices > 1:
-        rc = lib.gat_project_sliced(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
-                                    pp.a_src.data_ptr(), pp.c_src.data_ptr(),
-                                    pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f, slices,
-                                    p_wh, n, 0, heads, p_sd, stream)
-        if rc == 0:
-            rc = lib.gat_edge_aggregate_sliced(
-                csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, p_wh, n, slices,
-                pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, heads, f,
-                float(negative_slope), bias.data_ptr(), out.data_ptr(), hint, stream)
-            if rc:
-                _lib.check(rc, "gat_edge_aggregate_sliced")
-            return out
-        if rc != _lib.GAT_EUNSUPPORTED:  # nothing was launched: row-major below
-            _lib.check(rc, "gat_project_sliced")
-    rc = lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
-                         pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                         pp.c_dst.data_ptr(), heads, f, p_wh, hfp, p_ss, heads, p_sd, stream)
-    if rc:
-        _lib.check(rc, "gat_project")
-    rc = lib.gat_edge_aggregate(
-        csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0,
-        n, p_wh, hfp, p_ss, heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, heads, f,
-        int(concat), float(negative_slope), bias.data_ptr(), out.data_ptr(), 0, hint, stream)
-    if rc:
-        _lib.check(rc, "gat_edge_aggregate")
-    return out
+    plan = ForwardPlan(x, csr, heads, f, concat, negative_slope)
+    out = torch.empty(plan.n, plan.hf if concat else f, dtype=torch.float32, device=x.device)
+    plan.project(lib, x, pp)
+    return plan.edge(lib, csr, pp, bias, out)
 
 
 def score_activation_code(module) -> Tuple[int, float]:
@@ -464,7 +545,7 @@ class GraphAttentionLayer(torch.nn.Module):
 
     def forward(self, x, edge_index):
         x = _check_x(x, self.input_channels)
-        csr = get_csr(edge_index, x.size(0))
+        csr = get_csr(edge_index, x.size(0), x.device)
         p = float(self.dropout_val) if self.training else 0.0
         needs_grad = torch.is_grad_enabled() and (
             x.requires_grad or any(p_.requires_grad for p_ in self.parameters()))

@@ -1,0 +1,34 @@
+"""Kernel-choice knobs (A/B measurement in tools/ and the variant tests).
+
+The GAT_* environment variables are read ONCE, when this module is imported
+(and by the HIP library at its first launch), never per forward.  Tools and
+tests that switch variants inside one process call ``reload()`` after
+changing the environment; it re-reads the Python-side knobs and asks the
+library for a new snapshot (``gat_tuning_reload``).  No knob changes results
+beyond fp32 summation order; the defaults are the measured-fastest choices.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+# knobs read on the Python side of the boundary
+PY_KNOBS = ("GAT_WH_SLICES", "GAT_EDGE_ORDER", "GAT_HUB_SPLIT", "GAT_HUB_SEG")
+
+_values: Dict[str, Optional[str]] = {}
+
+
+def reload() -> None:
+    """Re-read the environment (Python knobs and the library's snapshot)."""
+    global _values
+    _values = {k: os.environ.get(k) for k in PY_KNOBS}
+    from . import _lib
+    if _lib.is_loaded():
+        _lib.load().gat_tuning_reload()
+
+
+def get(name: str) -> Optional[str]:
+    return _values.get(name)
+
+
+_values = {k: os.environ.get(k) for k in PY_KNOBS}

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 3
+#define GAT_ABI_VERSION 4
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -49,6 +49,14 @@ extern "C" {
 
 /* ABI version of the loaded library (== GAT_ABI_VERSION). */
 int gat_abi_version(void);
+
+/*
+ * Re-read the GAT_* kernel-choice environment variables (A/B knobs used by
+ * tools/ and the tests; never needed for correct results).  The library reads
+ * them once, at its first launch; this call takes a new snapshot.  Not safe
+ * to call while another thread launches through the library.
+ */
+int gat_tuning_reload(void);
 
 /*
  * Packed node-table layout for (heads, f): row stride `ld` floats and column
@@ -148,6 +156,55 @@ int gat_edge_aggregate_sliced(const int* rowptr, const int* col, const int* row_
                               const float* s_dst, int heads, int f, float negative_slope,
                               const float* bias, float* out, int edges_per_row_hint,
                               void* stream);
+
+/*
+ * Segmented edge aggregation: the same arithmetic as gat_edge_aggregate /
+ * gat_edge_aggregate_sliced (GAT.py:53-67, + bias GAT.py:54), over a SEGMENT
+ * of each row's in-edges, with the online-softmax state carried in memory.
+ * Replaces nothing new in the reference: it is the same segmented softmax
+ * (PyG utils.softmax, GAT.py:60) and scatter-add (aggr='add'), regrouped so
+ * that (a) the multi-GPU forward can run one pass per all-gather chunk while
+ * the next chunk is in flight, and (b) one very long row (a hub) can be cut
+ * into segments that run in parallel and are combined by gat_edge_merge.
+ *   seg_begin/seg_end  CSR positions: the segment of row i is
+ *                [seg_begin[k], seg_end[k]) with k = i, or k = the schedule
+ *                position (row_order index) when seg_by_pos != 0; state rows
+ *                are indexed by the same k
+ *   wh, ld_wh    slices == 1: row-major Wh-only table [.., ld_wh]
+ *   wh, n_table  slices > 1: column planes as gat_edge_aggregate_sliced
+ *                (plane g at wh + g * n_table * heads*f/slices)
+ *   st_acc       [.., round_up(heads*f, 4)] un-normalised accumulators
+ *   st_ml        [.., 2*heads]: per head, the running max (log2 units) then the sum
+ *   flags        GAT_SEG_LOAD: start from the stored state (else from empty);
+ *                GAT_SEG_STORE: every row stores its state (else writes the
+ *                normalised row, + bias, to out)
+ *   store_rows   with seg_by_pos and without GAT_SEG_STORE: the rows at schedule
+ *                positions < store_rows store their state (the segments of
+ *                split hub rows, scheduled first) and the others write their
+ *                output; 0 otherwise
+ * LeakyReLU with slope in [0, 1], f % 4 == 0, f/4 a power of two (the fused
+ * source score: a_src, c_src required); concat or head mean (slices == 1).
+ */
+#define GAT_SEG_LOAD 1
+#define GAT_SEG_STORE 2
+int gat_edge_aggregate_seg(const int* seg_begin, const int* seg_end, int seg_by_pos,
+                           const int* col, const int* row_order, int row_begin, int row_end,
+                           const float* wh, int ld_wh, int n_table, int slices,
+                           const float* a_src, const float* c_src, const float* s_dst, int heads,
+                           int f, int concat, float negative_slope, float* st_acc, float* st_ml,
+                           int flags, int store_rows, const float* bias, float* out,
+                           int edges_per_row_hint, void* stream);
+
+/*
+ * Combine split hub rows: hub k (target row hub_rows[k]) has segment states
+ * [seg_ptr[k], seg_ptr[k+1]) in st_acc / st_ml (written by
+ * gat_edge_aggregate_seg with seg_by_pos and GAT_SEG_STORE).  Writes the row's
+ * output (+ bias; concat or head mean), and optionally lse [.., heads] and
+ * y_heads [.., heads*f] as gat_edge_aggregate_ex does.
+ */
+int gat_edge_merge(const int* hub_rows, const int* seg_ptr, int n_hub, const float* st_acc,
+                   const float* st_ml, int heads, int f, int concat, const float* bias,
+                   float* out, float* lse, float* y_heads, void* stream);
 
 /* Workspace bytes gat_csr_build needs for (num_edges, num_nodes). */
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);

@@ -35,8 +35,8 @@ The reference cannot run unchanged here (``torch_geometric`` is not installed).
 ``tests/golden/make_golden.py`` runs the reference's own ``GAT.py`` with the
 three PyG entry points restated in ``tests/golden/pyg_restated`` and commits its
 outputs as fixtures; ``tests/test_oracle_golden.py`` checks this oracle against
-them, and ``tests/test_known_answer.py`` checks both against hand-derived
-closed-form values.  The PyG semantics themselves are restated, not run: see
+them, and its ``test_known_answer_closed_form`` checks both against a float64
+pure-Python closed form on the hand-checkable graphs.  The PyG semantics themselves are restated, not run: see
 DESIGN.md "Oracle and parity".
 """
 from __future__ import annotations

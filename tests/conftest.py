@@ -33,3 +33,31 @@ def load_golden(name):
     return dict(meta=meta, x=torch.from_numpy(z["x"].copy()),
                 edge_index=torch.from_numpy(z["edge_index"].copy()),
                 out=torch.from_numpy(z["out"].copy()), state=ordered)
+
+
+def _reload_tuning():
+    from atmlgraphattentionnetworks_amd import tuning
+    tuning.reload()
+
+
+@pytest.fixture(autouse=True)
+def _tuning_follows_env(monkeypatch):
+    """The library reads its GAT_* A/B knobs once (atmlgraphattentionnetworks_amd.tuning);
+    a test that switches variants with monkeypatch.setenv/delenv gets a fresh
+    snapshot after each change, and the original one back at teardown."""
+    orig_set, orig_del = monkeypatch.setenv, monkeypatch.delenv
+
+    def setenv(name, value, prepend=None):
+        orig_set(name, value, prepend)
+        if name.startswith("GAT_"):
+            _reload_tuning()
+
+    def delenv(name, raising=True):
+        orig_del(name, raising)
+        if name.startswith("GAT_"):
+            _reload_tuning()
+
+    monkeypatch.setenv, monkeypatch.delenv = setenv, delenv
+    yield
+    monkeypatch.undo()
+    _reload_tuning()

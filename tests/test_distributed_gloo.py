@@ -1,8 +1,9 @@
 """Node-range partitioned forward (atmlgraphattentionnetworks_amd/distributed.py)
 on CPU with gloo, world_size 2 and 3: edge-balanced partition, global->table-row
-remap, the in-place all-gather of the packed [Wh | s_src] table, local edge
-pass, output gather — with CPU stand-ins for the two HIP kernels (the kernels
-themselves are checked on the GPU).  The gathered output must equal the
+remap into the chunked table, the in-place asynchronous all-gather per chunk,
+the edge passes with the softmax state carried between them, output gather —
+with CPU stand-ins for the two HIP kernels (the kernels themselves are checked
+on the GPU, tests/test_gpu_distributed.py).  The gathered output must equal the
 oracle's full-graph forward."""
 import os
 import socket
@@ -17,66 +18,89 @@ from oracle import gat_layer_forward_from_state, init_reference_params
 
 
 class CpuOps:
-    """Test-only CPU restatements of gat_project / gat_edge_aggregate on the
-    same packed table layout the HIP path uses."""
+    """Test-only CPU restatements of the two shard kernels on the same blocked
+    table layout (distributed.TableLayout) the HIP path uses: the projection
+    into a rank's chunk block, and one segmented edge pass with the online-
+    softmax state (m, l, acc) carried between passes."""
 
     @staticmethod
-    def alloc_table(n, heads, f, device, packed=True, wh_only=False, slices=1):
-        from atmlgraphattentionnetworks_amd.layer import alloc_table
-        if slices > 1:
-            return alloc_table(n, heads, f, device, slices=slices)
-        if wh_only or packed:
-            return alloc_table(n, heads, f, device, packed=packed, wh_only=wh_only)
+    def project_rows(x, pp, heads, f, layout, table, offset, s_dst, s_scratch):
         hf = heads * f
-        from atmlgraphattentionnetworks_amd.layer import NodeTable
-        wh = torch.zeros(n, (hf + 3) // 4 * 4)
-        s_src = torch.zeros(n, heads)
-        return NodeTable(wh, wh.size(1), s_src, heads)
-
-    @staticmethod
-    def _row_major(table):
-        """[n, hf] view of the table's Wh (a copy for the sliced planes)."""
-        if table.slices > 1:
-            s, n, sw = table.wh.shape
-            return table.wh.permute(1, 0, 2).reshape(n, s * sw)
-        return table.wh
-
-    @staticmethod
-    def project(x, pp, heads, f, table, s_dst):
-        hf = heads * f
+        n = x.size(0)
         wh = x @ pp.w.T + pp.b
-        if table.slices > 1:  # plane g holds columns [g*sw, (g+1)*sw)
-            table.wh[:] = wh.view(wh.size(0), table.slices, -1).permute(1, 0, 2)
+        v = wh.view(n, heads, f)
+        B, W, S = layout.block_rows, layout.width, layout.slices
+        blk = table[offset:offset + layout.block_floats]
+        if layout.kind == "planes":  # plane g holds columns [g*W, (g+1)*W)
+            blk.view(S, B, W)[:, :n] = wh.view(n, S, W).permute(1, 0, 2)
         else:
-            table.wh[:, :hf] = wh
-        v = wh.view(-1, heads, f)
-        if table.s_src is not None:
-            table.s_src[:, :heads] = (v * pp.a_src.view(heads, f)).sum(-1) + pp.c_src
-        s_dst[:] = (v * pp.a_dst.view(heads, f)).sum(-1) + pp.c_dst
+            rows = blk.view(B, W)
+            rows[:n, :hf] = wh
+            if layout.kind == "packed":
+                rows[:n, layout.s_off:layout.s_off + heads] = \
+                    (v * pp.a_src.view(heads, f)).sum(-1) + pp.c_src
+        s_dst[:n] = (v * pp.a_dst.view(heads, f)).sum(-1) + pp.c_dst
 
     @staticmethod
-    def edge_aggregate(csr, table, s_dst, heads, f, concat, bias, slope, out, pp=None):
+    def _gather(layout, table, trows, hf):
+        W = layout.width
+        t = table.view(-1, W)
+        if layout.kind == "planes":
+            return torch.cat([t[trows + g * layout.block_rows] for g in range(layout.slices)], 1)
+        return t[trows, :hf]
+
+    @staticmethod
+    def edge_pass(local, c, layout, table, s_dst, pp, bias, heads, f, concat, act, param, out,
+                  st_acc, st_ml, flags):
+        from atmlgraphattentionnetworks_amd import _lib
         hf = heads * f
-        rp = csr.rowptr.long()
-        deg = rp[1:] - rp[:-1]
-        dst = torch.repeat_interleave(torch.arange(csr.num_nodes), deg)
-        src = csr.col.long()
-        whf = CpuOps._row_major(table)
-        if table.s_src is None:  # Wh-only table: recompute s_src from the Wh rows (fused score)
-            assert pp is not None
-            s_src = (whf[:, :hf].view(-1, heads, f) * pp.a_src.view(heads, f)).sum(-1) \
-                + pp.c_src
+        n = local.num_nodes
+        if layout.kind == "packed":
+            assert flags == 0
+            lo = local.rowptr[:-1].long()
+            hi = local.rowptr[1:].long()
         else:
-            s_src = table.s_src[:, :heads]
-        e = torch.nn.functional.leaky_relu(s_dst[dst] + s_src[src], slope)
-        m = torch.full((csr.num_nodes, heads), float("-inf")).scatter_reduce(
-            0, dst.view(-1, 1).expand_as(e), e, "amax", include_self=False)
-        p = (e - m[dst]).exp()
-        l = torch.zeros(csr.num_nodes, heads).index_add_(0, dst, p)
-        a = p / (l[dst] + 1e-16)
-        msg = whf[src, :hf].view(-1, heads, f) * a.unsqueeze(-1)
-        y = torch.zeros(csr.num_nodes, heads, f).index_add_(0, dst, msg)
-        out[:] = (y.reshape(csr.num_nodes, hf) if concat else y.mean(1)) + bias
+            lo, hi = local.seg[c].long(), local.seg[c + 1].long()
+        deg = hi - lo
+        dst = torch.repeat_interleave(torch.arange(n), deg)
+        pos = torch.cat([torch.arange(int(a), int(b)) for a, b in zip(lo, hi)]) \
+            if n else torch.zeros(0, dtype=torch.long)
+        src = local.col[pos].long()
+        whs = CpuOps._gather(layout, table, src, hf)
+        if layout.kind == "packed":
+            s_src = table.view(-1, layout.width)[src, layout.s_off:layout.s_off + heads]
+        else:
+            s_src = (whs.view(-1, heads, f) * pp.a_src.view(heads, f)).sum(-1) + pp.c_src
+        z = s_dst[dst] + s_src
+        if act == _lib.GAT_ACT_LEAKY_RELU:
+            e = torch.nn.functional.leaky_relu(z, param)
+        elif act == _lib.GAT_ACT_TANH:
+            e = torch.tanh(z)
+        else:
+            assert act == _lib.GAT_ACT_LOG_SIGMOID
+            e = torch.nn.functional.logsigmoid(z)
+        m_seg = torch.full((n, heads), float("-inf")).scatter_reduce(
+            0, dst.view(-1, 1).expand_as(e), e, "amax", include_self=True)
+        if flags & _lib.GAT_SEG_LOAD:
+            m_old, l_old = st_ml[:n, :heads], st_ml[:n, heads:]
+            acc_old = st_acc[:n, :hf].view(n, heads, f)
+        else:
+            m_old = torch.full((n, heads), float("-inf"))
+            l_old = torch.zeros(n, heads)
+            acc_old = torch.zeros(n, heads, f)
+        m = torch.maximum(m_old, m_seg)
+        ms = torch.where(torch.isinf(m), torch.zeros_like(m), m)  # safe shift
+        sc = torch.where(torch.isinf(m_old), torch.zeros_like(m), (m_old - ms).exp())
+        p = (e - ms[dst]).exp()
+        l = l_old * sc + torch.zeros(n, heads).index_add_(0, dst, p)
+        acc = acc_old * sc.unsqueeze(-1) + torch.zeros(n, heads, f).index_add_(
+            0, dst, whs.view(-1, heads, f) * p.unsqueeze(-1))
+        if flags & _lib.GAT_SEG_STORE:
+            st_ml[:n, :heads], st_ml[:n, heads:] = m, l
+            st_acc[:n, :hf] = acc.reshape(n, hf)
+            return out
+        y = acc / (l.unsqueeze(-1) + 1e-16)
+        out[:] = (y.reshape(n, hf) if concat else y.mean(1)) + bias
         return out
 
 
@@ -92,13 +116,19 @@ class _PP:
 
 
 class _Layer:
-    def __init__(self, state, H, F, concat):
+    def __init__(self, state, H, F, concat, act=None):
         self.num_heads, self.output_channels, self.concat = H, F, concat
         self.bias = state["bias"]
         self._pp = _PP(state, H)
+        self._act = act
 
     def packed(self):
         return self._pp
+
+    def score_activation(self):
+        from atmlgraphattentionnetworks_amd.layer import score_activation_code
+        return score_activation_code(self._act if self._act is not None
+                                     else torch.nn.LeakyReLU(0.2))
 
 
 def _case(n=400, e=5000, fin=12, H=4, F=8, concat=True, seed=3):
@@ -122,24 +152,41 @@ def _cpu_csr(ei, n):
                     torch.from_numpy(s[order].astype(np.int32)), n, len(s))
 
 
-def _worker(rank, world, port, exchange, concat, results, F=8, slices=None):
+def _act_module(name):
+    return {None: None, "lrelu0.3": torch.nn.LeakyReLU(0.3), "lrelu0.01": torch.nn.LeakyReLU(0.01),
+            "tanh": torch.nn.Tanh(), "logsigmoid": torch.nn.LogSigmoid()}[name]
+
+
+def _worker(rank, world, port, exchange, concat, results, F=8, slices=None, chunks=None,
+            act=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if slices is not None:
         os.environ["GAT_WH_SLICES"] = str(slices)
+        from atmlgraphattentionnetworks_amd import tuning
+        tuning.reload()
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from atmlgraphattentionnetworks_amd.distributed import ShardedGAT, gather_output
         x, ei, state = _case(concat=concat, F=F)
         H = 4
         csr = _cpu_csr(ei, x.size(0))
-        sh = ShardedGAT(_Layer(state, H, F, concat), csr, world, rank, exchange=exchange,
-                        ops=CpuOps)
+        module = _act_module(act)
+        sh = ShardedGAT(_Layer(state, H, F, concat, module), csr, world, rank,
+                        exchange=exchange, ops=CpuOps, chunks=chunks)
         results["wh_only"] = sh.wh_only
         results["slices"] = sh.slices
+        results["chunks"] = sh.chunks
         out = sh.forward(sh.local_x(x))
         full = gather_output(out, sh.bounds)
+        results["fused"] = sh.fused
         if rank == 0:
-            ref = gat_layer_forward_from_state(state, x, ei, H, concat)
+            if module is None:
+                ref = gat_layer_forward_from_state(state, x, ei, H, concat)
+            else:
+                from oracle import gat_layer_forward_differentiable
+                with torch.no_grad():
+                    ref = gat_layer_forward_differentiable(state, x, ei, H, concat,
+                                                           activation=module)
             results["max_diff"] = float((full - ref).abs().max())
             results["shape_ok"] = tuple(full.shape) == tuple(ref.shape)
             results["bounds"] = sh.bounds
@@ -160,13 +207,13 @@ def _free_port():
 @pytest.mark.parametrize("concat", [True, False])
 @pytest.mark.parametrize("F", [8, 6])
 def test_sharded_forward_matches_oracle(world, exchange, concat, F):
-    """F=8: the all-gather moves a Wh-only table (s_src recomputed from Wh);
-    F=6: the packed [Wh | s_src] table."""
+    """F=8: a Wh-only table (the edge kernel recomputes s_src from the row);
+    F=6: the packed [Wh | s_src] table (one pass, any score activation)."""
     mgr = mp.Manager()
     results = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), exchange, concat, results, F), nprocs=world,
              join=True)
-    assert results["wh_only"] == (exchange == "allgather" and F == 8)
+    assert results["wh_only"] == (F == 8)
     assert results["shape_ok"]
     assert results["max_diff"] < 1e-5, results["max_diff"]
     # edge-balanced: every rank within 10% of E'/P
@@ -187,16 +234,69 @@ def test_sharded_forward_sliced_table(world):
     assert results["max_diff"] < 1e-5, results["max_diff"]
 
 
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("chunks", [2, 3])
+@pytest.mark.parametrize("slices", [1, 2])
+@pytest.mark.parametrize("concat", [True, False])
+def test_sharded_forward_chunked_passes(world, chunks, slices, concat):
+    """The overlapped schedule: the table all-gathered in `chunks` asynchronous
+    chunks, the edge work in as many passes with the softmax state carried
+    between them (GAT_SEG_LOAD / GAT_SEG_STORE), on the Wh-only (slices=1) and
+    the 2-plane table."""
+    if slices == 2 and not concat:
+        pytest.skip("planes are a concat layout")
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), "allgather", concat, results, 8, slices, chunks),
+             nprocs=world, join=True)
+    assert results["chunks"] == chunks and results["slices"] == slices
+    assert results["shape_ok"]
+    assert results["max_diff"] < 1e-5, results["max_diff"]
+
+
+@pytest.mark.parametrize("act,concat,chunks", [("lrelu0.3", True, 2), ("lrelu0.01", False, 3),
+                                               ("tanh", True, None), ("logsigmoid", False, None)])
+def test_sharded_forward_score_activations(act, concat, chunks):
+    """The layer's own score activation reaches the shard kernels (it is not
+    the reference default 0.2): LeakyReLU slopes take the fused chunked path,
+    Tanh / LogSigmoid the packed [Wh | s_src] table in one pass."""
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), "allgather", concat, results, 8, None, chunks, act),
+             nprocs=2, join=True)
+    assert results["fused"] == act.startswith("lrelu")
+    assert results["shape_ok"]
+    assert results["max_diff"] < 1e-5, results["max_diff"]
+
+
 def test_partition_rows_edge_balanced():
-    from atmlgraphattentionnetworks_amd.distributed import partition_rows, remap_to_table
+    from atmlgraphattentionnetworks_amd.distributed import partition_rows
     deg = torch.tensor([1, 50, 1, 1, 1, 30, 1, 1, 20, 1], dtype=torch.int32)
     rowptr = torch.cat([torch.zeros(1, dtype=torch.int32), deg.cumsum(0).to(torch.int32)])
     b = partition_rows(rowptr, 3)
     assert b[0] == 0 and b[-1] == 10 and b == sorted(b)
-    col = torch.arange(10, dtype=torch.int32)
-    m = max(b[k + 1] - b[k] for k in range(3))
-    t = remap_to_table(col, b, m)
-    for k in range(3):
-        for n in range(b[k], b[k + 1]):
-            assert int(t[n]) == k * m + (n - b[k])
     assert partition_rows(rowptr, 1) == [0, 10]
+
+
+def test_table_layout_rows_and_chunks():
+    """Table rows of the blocked layout [chunks][world][slices][B][W]: rank p's
+    i-th row lands in chunk i // B at (c*world + p)*slices*B + i % B, and every
+    block / chunk range tiles the table exactly once."""
+    from atmlgraphattentionnetworks_amd.distributed import TableLayout
+    lay = TableLayout("planes", world=3, chunks=2, block_rows=64, slices=2, width=32)
+    assert lay.numel == 2 * 3 * 2 * 64 * 32
+    seen = set()
+    for p in range(3):
+        local = torch.arange(128)
+        rows = lay.row_of(torch.full_like(local, p), local)
+        for i, r in zip(local.tolist(), rows.tolist()):
+            c, ii = divmod(i, 64)
+            assert r == (c * 3 + p) * 128 + ii
+            assert int(lay.chunk_of_row(torch.tensor(r))) == c
+            seen.add(r)
+    assert len(seen) == 3 * 128
+    spans = sorted((lay.block_offset(c, p), lay.block_offset(c, p) + lay.block_floats)
+                   for c in range(2) for p in range(3))
+    assert spans[0][0] == 0 and spans[-1][1] == lay.numel
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert lay.chunk_range(1) == (3 * lay.block_floats, 6 * lay.block_floats)

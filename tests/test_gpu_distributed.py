@@ -1,8 +1,18 @@
-"""The sharded (node-range partitioned) forward's HIP path on ONE GPU: P
-ShardedGAT ranks in one process, the all-gather emulated by copying every
-rank's projected slot into every rank's packed table.  Covers the kernels on
-the packed [Wh | s_src] layout with remapped (table-row) column ids and row
-slices; the RCCL collective itself runs in bench.py --gpus N."""
+"""The node-partitioned forward's HIP kernels (distributed.py)
+on ONE GPU: ``distributed.emulate`` runs P ranks in one process — every
+rank's projection into its blocks of its own table, the all-gather emulated
+by block copies, every rank's edge passes with the softmax state carried
+between passes (gat_edge_aggregate_seg) — and the concatenated output must
+match the oracle (small graphs, BASELINE.json's configs in partitioned form)
+or the single-GPU forward (full size; that forward is itself checked against
+the oracle in test_gpu_parity.py / test_gpu_fullsize.py).
+
+Bar: |sharded - ref| <= 1e-5 + 1e-5 |ref| (fp32; the passes change the
+summation order only).  RCCL itself needs distinct GPUs: the multi-process
+path is rehearsed here with two ranks on cuda:0 exchanging through gloo
+(test_bench_two_ranks_shared_gpu), and runs over RCCL in the driver's
+multi-GPU bench.
+"""
 import pytest
 import torch
 
@@ -10,59 +20,147 @@ from oracle import gat_layer_forward_from_state, init_reference_params
 
 pytestmark = pytest.mark.gpu
 
+ATOL = RTOL = 1e-5
+DEV = torch.device("cuda", 0)
+
+
+def _layer(fin, F, H, concat, state, act=None):
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    from atmlgraphattentionnetworks_amd.layer import GraphAttentionLayerActivationTest
+    if act is None:
+        layer = GraphAttentionLayer(fin, F, num_heads=H, concat=concat)
+    else:
+        layer = GraphAttentionLayerActivationTest(fin, F, num_heads=H, concat=concat,
+                                                  activation_function=act)
+    layer.load_state_dict(state)
+    return layer.to(DEV).eval()
+
+
+def _small_case(concat, n=3000, e=60000, fin=50, H=8, F=8, seed=1):
+    from atmlgraphattentionnetworks_amd.synthetic import uniform_graph
+    state = init_reference_params(fin, F, H, concat, seed=seed)
+    state["bias"] = torch.randn(state["bias"].shape)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(seed)
+    x = torch.randn(n, fin, generator=g, device=DEV)
+    ei = uniform_graph(n, e, seed=4, device=DEV)
+    return state, x, ei
+
 
 @pytest.mark.parametrize("P", [2, 4, 8])
 @pytest.mark.parametrize("exchange", ["allgather", "replicate"])
 @pytest.mark.parametrize("concat", [True, False])
 @pytest.mark.parametrize("table", ["default", "row_major"])
-def test_sharded_hip_path_matches_single_gpu(P, exchange, concat, table, monkeypatch):
-    """table=default: at 21 edges per row the concat all-gather table is 2
-    column planes (one all-gather per plane); row_major: GAT_WH_SLICES=1."""
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_sharded_hip_path_matches_oracle(P, exchange, concat, table, chunks, monkeypatch):
+    """table=default: at 21 edges per row the concat table is 2 column planes;
+    row_major: GAT_WH_SLICES=1 (Wh-only rows).  chunks=3: the all-gather in 3
+    chunks and 3 edge passes carrying (m, l, acc)."""
     if table == "row_major":
         monkeypatch.setenv("GAT_WH_SLICES", "1")
     else:
         monkeypatch.delenv("GAT_WH_SLICES", raising=False)
-    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
-    from atmlgraphattentionnetworks_amd.distributed import ShardedGAT
-    from atmlgraphattentionnetworks_amd.synthetic import uniform_graph
-    dev = torch.device("cuda", 0)
-    n, e, fin, H, F = 3000, 60000, 50, 8, 8
-    state = init_reference_params(fin, F, H, concat, seed=1)
-    state["bias"] = torch.randn(state["bias"].shape)
-    layer = GraphAttentionLayer(fin, F, num_heads=H, concat=concat)
-    layer.load_state_dict(state)
-    layer = layer.to(dev).eval()
-    g = torch.Generator(device=dev)
-    g.manual_seed(1)
-    x = torch.randn(n, fin, generator=g, device=dev)
-    ei = uniform_graph(n, e, seed=4, device=dev)
-    csr = get_csr(ei, n)
+    if exchange == "replicate" and chunks > 1:
+        pytest.skip("replicate has no collective to overlap")
+    from atmlgraphattentionnetworks_amd import get_csr
+    from atmlgraphattentionnetworks_amd.distributed import ShardedGAT, emulate
+    state, x, ei = _small_case(concat)
+    layer = _layer(50, 8, 8, concat, state)
+    csr = get_csr(ei, x.size(0))
     with torch.no_grad():
-        ranks = [ShardedGAT(layer, csr, P, r, exchange=exchange) for r in range(P)]
+        sh = ShardedGAT(layer, csr, P, 0, exchange=exchange, chunks=chunks)
+        assert sh.slices == (2 if concat and table == "default" else 1)
         if exchange == "allgather":
-            assert ranks[0].slices == (2 if concat and table == "default" else 1)
-        for sh in ranks:
-            sh.phase_project(sh.local_x(x))
-        if exchange == "allgather":
-            m = ranks[0].rows_per_part
-            for dst in ranks:
-                for src in ranks:
-                    sl = slice(src.rank * m, (src.rank + 1) * m)
-                    if dst.slices > 1:  # [planes, rows, plane width]
-                        dst.table.buf[:, sl] = src.table.buf[:, sl]
-                    else:
-                        dst.table.buf[sl] = src.table.buf[sl]
-        outs = [sh.phase_edges().clone() for sh in ranks]
-    full = torch.cat(outs).cpu()
-    ref = gat_layer_forward_from_state(state, x.cpu(), ei.cpu(), H, concat)
-    torch.testing.assert_close(full, ref, atol=1e-5, rtol=1e-5)
+            assert sh.chunks == chunks
+        full = emulate(layer, csr, x, P, exchange=exchange, chunks=chunks).cpu()
+    ref = gat_layer_forward_from_state(state, x.cpu(), ei.cpu(), 8, concat)
+    torch.testing.assert_close(full, ref, atol=ATOL, rtol=RTOL)
 
 
-def test_bench_weak_scaling_two_ranks_one_line(tmp_path):
-    """bench.py's multi-GPU path end to end with 2 torchrun ranks sharing cuda:0
-    (GAT_BENCH_SHARE_GPU0; the pool's boxes have one GPU): gloo barriers, the
-    max-over-ranks timing, and exactly one JSON line on rank 0's stdout.  The
-    RCCL strong-scaling probe needs distinct GPUs and is skipped here."""
+@pytest.mark.parametrize("act_name,concat,chunks", [("lrelu0.3", True, 2), ("lrelu0.01", False, 3),
+                                                    ("relu", True, 2), ("tanh", True, 1),
+                                                    ("logsigmoid", False, 1)])
+def test_sharded_score_activation(act_name, concat, chunks):
+    """The layer's score activation reaches the shard kernels: LeakyReLU(0.3),
+    LeakyReLU(0.01) and ReLU on the fused chunked path, Tanh / LogSigmoid on the
+    packed [Wh | s_src] table (one pass)."""
+    from atmlgraphattentionnetworks_amd import get_csr
+    from atmlgraphattentionnetworks_amd.distributed import emulate
+    from oracle import gat_layer_forward_differentiable
+    act = {"lrelu0.3": torch.nn.LeakyReLU(0.3), "lrelu0.01": torch.nn.LeakyReLU(0.01),
+           "relu": torch.nn.ReLU(), "tanh": torch.nn.Tanh(),
+           "logsigmoid": torch.nn.LogSigmoid()}[act_name]
+    state, x, ei = _small_case(concat, n=2000, e=40000)
+    layer = _layer(50, 8, 8, concat, state, act)
+    csr = get_csr(ei, x.size(0))
+    with torch.no_grad():
+        full = emulate(layer, csr, x, 4, chunks=chunks).cpu()
+        ref = gat_layer_forward_differentiable(state, x.cpu(), ei.cpu(), 8, concat,
+                                               activation=act)
+    torch.testing.assert_close(full, ref, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_arxiv_full_size_partitioned(P, chunks):
+    """BASELINE.json configs[3] (ogbn-arxiv scale: N=169,343, E=1,166,243,
+    Fin=128, H=8, F=8) node-partitioned over P ranks, at full size: equals
+    the single-GPU forward (which test_gpu_fullsize.py checks in full against
+    the oracle)."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
+    from atmlgraphattentionnetworks_amd.distributed import emulate
+    from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
+    w = WORKLOADS["arxiv"]
+    x, ei = make_inputs(w, DEV)
+    torch.manual_seed(0)
+    layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
+                                concat=w.concat).to(DEV).eval()
+    with torch.no_grad():
+        layer.bias.normal_()
+        one = layer(x, ei)
+        full = emulate(layer, get_csr(ei, x.size(0)), x, P, chunks=chunks)
+    torch.testing.assert_close(full, one, atol=ATOL, rtol=RTOL)
+
+
+def test_reddit_scale_partitioned_p8():
+    """BASELINE.json configs[4] (Reddit scale, 114.8M edges) node-partitioned
+    over 8 ranks with the all-gather in 4 chunks: every row equals the
+    single-GPU forward, and 64 sampled rows equal the oracle evaluated on
+    their complete in-edge sets."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
+    from atmlgraphattentionnetworks_amd.distributed import ShardedGAT, emulate
+    from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
+    w = WORKLOADS["reddit"]
+    x, ei = make_inputs(w, DEV)
+    state = init_reference_params(w.in_channels, w.out_channels, w.heads, w.concat, seed=0)
+    state["bias"] = torch.randn(state["bias"].shape)
+    layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
+                                concat=w.concat)
+    layer.load_state_dict(state)
+    layer = layer.to(DEV).eval()
+    csr = get_csr(ei, x.size(0))
+    with torch.no_grad():
+        sh = ShardedGAT(layer, csr, 8, 3, chunks=4)
+        assert sh.chunks == 4 and sh.slices == 2
+        del sh
+        one = layer(x, ei)
+        full = emulate(layer, csr, x, 8, chunks=4)
+    torch.testing.assert_close(full, one, atol=ATOL, rtol=RTOL)
+    g = torch.Generator(device="cpu")
+    g.manual_seed(321)
+    rows = torch.randperm(x.size(0), generator=g)[:64].to(DEV)
+    keep = torch.isin(ei[1], rows)
+    sub = ei[:, keep].cpu()
+    ref = gat_layer_forward_from_state(state, x.cpu(), sub, w.heads, w.concat)
+    torch.testing.assert_close(full[rows].cpu(), ref[rows.cpu()], atol=ATOL, rtol=RTOL)
+
+
+def test_bench_two_ranks_shared_gpu():
+    """bench.py --gpus 2 end to end with 2 torchrun ranks on cuda:0
+    (GAT_BENCH_SHARE_GPU0; the all-gather staged through gloo because RCCL
+    refuses two ranks on one device): the chunked shared-graph step, the
+    max-over-ranks timing, the in-run check of the gathered output against the
+    single-GPU forward, and exactly one JSON line on rank 0's stdout."""
     import json
     import os
     import socket
@@ -75,11 +173,15 @@ def test_bench_weak_scaling_two_ranks_one_line(tmp_path):
     env = dict(os.environ, GAT_BENCH_SHARE_GPU0="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--no-strong-probe", "--steps", "10", "--warmup", "3"]
+           "--dist-workloads", "arxiv", "--steps", "6", "--warmup", "2"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
-    assert d["steps"] == 10 and d["unit"] == "edges/s"
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
+    assert d["steps"] == 6 and d["unit"] == "edges/s"
+    arx = d["workloads"]["arxiv"]
+    assert arx["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * arx["check"]["max_abs_ref"]
+    assert set(arx["chunk_trials_ms"]) == {"1", "2", "4"} or set(arx["chunk_trials_ms"]) == {1, 2, 4}
+    assert d["ppi_blocks_data_parallel"]["value"] > 0

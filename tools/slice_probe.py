@@ -17,6 +17,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import torch  # noqa: E402
 
+from atmlgraphattentionnetworks_amd import tuning  # noqa: E402
+
 from tune_edge import time_fn  # noqa: E402
 
 
@@ -115,6 +117,7 @@ def main():
                     os.environ["GAT_EDGE_U"] = str(u)
                 else:
                     os.environ.pop("GAT_EDGE_U", None)
+                tuning.reload()
                 wh, sd, _ = prepared[s]
                 out = torch.empty(n, hf, device=dev)
                 res[(s, v, u, o, d)].append(time_fn(edge_fn(s, wh, sd, out), args.iters))
@@ -123,12 +126,15 @@ def main():
             os.environ.pop("GAT_EDGE_U", None)
             os.environ.pop("GAT_EDGE_PIPE", None)
             os.environ.pop("GAT_EDGE_LDS", None)
+            tuning.reload()
             for s in slices:
                 pres[s].append(time_fn(prepared[s][2], args.iters))
                 os.environ["GAT_WH_SLICES"] = str(s)
+                tuning.reload()
                 fres[s].append(time_fn(lambda: gat_forward(x, csr, pp, bias, H, F, True, 0.2),
                                        args.iters))
             os.environ.pop("GAT_WH_SLICES", None)
+            tuning.reload()
     alg = edge_kernel_bytes(n, csr.num_edges, H, F, True)
     ref = outs[variants[0]]
     summary = {}

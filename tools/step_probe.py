@@ -17,6 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
+from atmlgraphattentionnetworks_amd import tuning  # noqa: E402
+
 
 def parse_variants(spec):
     out = {}
@@ -74,6 +76,7 @@ def main():
                 for k in knobs:
                     os.environ.pop(k, None)
                 os.environ.update(env)
+                tuning.reload()
                 slices = wh_slices(H, F, w.concat, layer.negative_slope, csr.num_edges // n)
                 table = alloc_table(n, H, F, dev, slices=slices)
                 table64 = alloc_table(64, H, F, dev, slices=slices)

@@ -17,6 +17,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 import torch  # noqa: E402
 
+from atmlgraphattentionnetworks_amd import tuning  # noqa: E402
+
 from step_probe import parse_variants  # noqa: E402
 
 
@@ -53,6 +55,7 @@ def main():
             for k in knobs:
                 os.environ.pop(k, None)
             os.environ.update(env)
+            tuning.reload()
             torch.manual_seed(1)
             for _ in range(2):
                 step()

@@ -15,6 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
+from atmlgraphattentionnetworks_amd import tuning  # noqa: E402
+
 EDGE_VARIANTS = {
     "generic": {"GAT_EDGE_KERNEL": "generic"},
     "gather_v1": {"GAT_EDGE_SCORE": "gather"},
@@ -30,7 +32,7 @@ EDGE_VARIANTS = {
 }
 REF_MM = True  # also time torch.mm(x, W^T) (hipBLASLt) as a projection reference point
 PROJ_VARIANTS = {"generic": {"GAT_PROJ_KERNEL": "lds"}, "tiled": {"GAT_PROJ_KERNEL": "tiled"},
-                 "direct": {"GAT_PROJ_KERNEL": "direct"}, "wk": {}}
+                 "wk": {}}
 
 
 def set_env(d):
@@ -38,6 +40,7 @@ def set_env(d):
               "GAT_EDGE_ORDER"):
         os.environ.pop(k, None)
     os.environ.update(d)
+    tuning.reload()
 
 
 def time_fn(fn, iters, reps=3):
