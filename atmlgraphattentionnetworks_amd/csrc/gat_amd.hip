@@ -533,6 +533,277 @@ __global__ __launch_bounds__(256) void k_project_pipe2(
 }
 
 // ---------------------------------------------------------------------------
+// Projection on the bf16 matrix cores with split operands (Fin > 64: arxiv,
+// Reddit).  gfx950's fp32 MFMA runs at the fp32 vector rate (1/16 of bf16), so
+// the fp32 kernel above is MFMA-bound at Reddit scale (18 GFLOP: 115 us at
+// peak).  Here every fp32 operand is split EXACTLY into three bf16 terms by
+// round-to-nearest (x = x1 + x2 + x3: x1 = bf16(x), x2 = bf16(x - x1),
+// x3 = x - x1 - x2, which has <= 8 significant bits, so bf16(x3) is exact),
+// and x.w = sum over the six products x_i w_j with i + j <= 4 (bf16 x bf16
+// products are exact in fp32).  The dropped terms x2 w3 + x3 w2 + x3 w3 are
+// below 2^-24 |x w| each: fp32 rounding level, like the fp32 MFMA's own k-ordered
+// chain.  Six v_mfma_f32_16x16x32_bf16 (16 cycles each) replace eight
+// v_mfma_f32_16x16x4_f32 (32 cycles each) per 32-deep k step: 2.7x the
+// product rate.  x1.w1 accumulates in `acc`, the five correction products in
+// `cor` (summed at the end), so the small terms are not rounded against the
+// large running sum at every step.
+//
+// Block: 64 rows x BN columns, one 16-row group per wave; 64-deep K chunks
+// through LDS as k_project_pipe2, but with TWO chunks' loads in flight (a
+// register double buffer): with the MFMA phase 2.7x shorter, one chunk in
+// flight left the loads exposed (the 128-row, one-ahead form of this kernel
+// ran Reddit in 196 us, 2.9 TB/s of x).
+// x stays fp32 in LDS and each lane splits its own A fragment (8 consecutive k
+// of one row) after reading it — every x element is split exactly once; W is
+// split once per chunk at the LDS write, into three bf16 planes the waves
+// share.  Fragment maps (cdna_hip_programming.md §3): lane l holds
+// A[row l&15][k 8(l>>4)..+8] and B[k 8(l>>4)..+8][col l&15]; C/D as the fp32
+// form (col l&15, rows 4(l>>4)+i), so the epilogue is k_project_pipe2's.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// exact three-way bf16 split of a float pair (round to nearest at each level)
+__device__ __forceinline__ void split3_pair(f32x2 v, bf16x2& p1, bf16x2& p2, bf16x2& p3) {
+    p1 = __builtin_convertvector(v, bf16x2);
+    const f32x2 r1 = v - __builtin_convertvector(p1, f32x2);
+    p2 = __builtin_convertvector(r1, bf16x2);
+    const f32x2 r2 = r1 - __builtin_convertvector(p2, f32x2);
+    p3 = __builtin_convertvector(r2, bf16x2);
+}
+
+__device__ __forceinline__ void split3_x8(f32x4 a, f32x4 b, bf16x8& h1, bf16x8& h2, bf16x8& h3) {
+    bf16x2 p1[4], p2[4], p3[4];
+    split3_pair(f32x2{a.x, a.y}, p1[0], p2[0], p3[0]);
+    split3_pair(f32x2{a.z, a.w}, p1[1], p2[1], p3[1]);
+    split3_pair(f32x2{b.x, b.y}, p1[2], p2[2], p3[2]);
+    split3_pair(f32x2{b.z, b.w}, p1[3], p2[3], p3[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        h1[2 * i] = p1[i][0];
+        h1[2 * i + 1] = p1[i][1];
+        h2[2 * i] = p2[i][0];
+        h2[2 * i + 1] = p2[i][1];
+        h3[2 * i] = p3[i][0];
+        h3[2 * i + 1] = p3[i][1];
+    }
+}
+
+template <int NT, int LW, int RG, int PD>
+__global__ __launch_bounds__(256) void k_project_x3(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
+    float* __restrict__ s_dst, int slice_w, long long slice_stride) {
+    // RG 16-row groups per wave, 4 waves: BM = 64 RG rows per block
+    constexpr int BK = 64, BN = NT * 16, NTH = 256, BM = 64 * RG;
+    constexpr int XS = BK + 4, WSB = BK + 8, OS = BN + 4;
+    constexpr int XL = BM * BK / (NTH * LW);  // x loads per thread per chunk
+    constexpr int WL = BN * BK / (NTH * LW) > 0 ? BN * BK / (NTH * LW) : 1;  // W loads
+    static_assert(BN * BK % (NTH * LW) == 0 || BN * BK < NTH * LW, "W chunk split");
+    static_assert(OS <= XS, "the output tile reuses the x tile");
+    using vec = typename std::conditional<LW == 4, f32x4,
+                typename std::conditional<LW == 2, f32x2, float>::type>::type;
+    __shared__ __attribute__((aligned(16))) __bf16 wsb[3][BN * WSB];
+    __shared__ __attribute__((aligned(16))) float xsm[BM * XS];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int blk0 = blockIdx.x * BM;
+    const int row0 = blk0 + w * 16 * RG;  // wave w owns rows [16 RG w, 16 RG (w + 1))
+    f32x4 acc[RG][NT], cor[RG][NT];
+#pragma unroll
+    for (int g = 0; g < RG; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] = cor[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // PD chunks of loads in flight (PD = 2: a register double buffer,
+    // statically indexed)
+    vec xa_[XL], wa_[WL], xb_[PD == 2 ? XL : 1], wb_[PD == 2 ? WL : 1];
+    auto load_chunk = [&](int k0, vec (&xn)[XL], vec (&wn)[WL]) {
+        // element e = (tid + 256 q) * LW -> row e / 64, k e % 64 (coalesced rows);
+        // clamped, in-bounds addresses past n / fin (zeroed W meets them)
+#pragma unroll
+        for (int q = 0; q < XL; ++q) {
+            const int e = (tid + NTH * q) * LW;
+            const int r = min(blk0 + e / BK, n - 1);
+            const int k = min(k0 + e % BK, fin - LW);
+            xn[q] = *reinterpret_cast<const vec*>(X + (size_t)r * fin + k);
+        }
+#pragma unroll
+        for (int q = 0; q < WL; ++q) {
+            const int e = (tid + NTH * q) * LW;
+            const int nn = min(e / BK, HF - 1);  // (e past the chunk: a clamped dummy)
+            const int k = min(k0 + e % BK, fin - LW);
+            wn[q] = *reinterpret_cast<const vec*>(W + (size_t)nn * fin + k);
+        }
+    };
+    // x chunk to LDS as fp32; W chunk split into three bf16 planes
+    auto stage = [&](int k0, const vec (&xn)[XL], const vec (&wn)[WL]) {
+#pragma unroll
+        for (int q = 0; q < XL; ++q) {
+            const int e = (tid + NTH * q) * LW;
+            *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) = xn[q];
+        }
+#pragma unroll
+        for (int q = 0; q < WL; ++q) {
+            const int e = (tid + NTH * q) * LW;
+            const bool ok = e / BK < HF && k0 + e % BK < fin && e < BN * BK;
+            const int o = min(e / BK, BN - 1) * WSB + e % BK;
+            if constexpr (LW == 1) {
+                bf16x2 p1, p2, p3;
+                split3_pair(f32x2{ok ? wn[q] : 0.f, 0.f}, p1, p2, p3);
+                wsb[0][o] = p1[0];
+                wsb[1][o] = p2[0];
+                wsb[2][o] = p3[0];
+            } else if constexpr (LW == 2) {
+                bf16x2 p1, p2, p3;
+                split3_pair(ok ? wn[q] : f32x2{0.f, 0.f}, p1, p2, p3);
+                *reinterpret_cast<bf16x2*>(&wsb[0][o]) = p1;
+                *reinterpret_cast<bf16x2*>(&wsb[1][o]) = p2;
+                *reinterpret_cast<bf16x2*>(&wsb[2][o]) = p3;
+            } else {
+                const f32x4 v = ok ? wn[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+                bf16x2 p1a, p2a, p3a, p1b, p2b, p3b;
+                split3_pair(f32x2{v.x, v.y}, p1a, p2a, p3a);
+                split3_pair(f32x2{v.z, v.w}, p1b, p2b, p3b);
+                *reinterpret_cast<bf16x4*>(&wsb[0][o]) = bf16x4{p1a[0], p1a[1], p1b[0], p1b[1]};
+                *reinterpret_cast<bf16x4*>(&wsb[1][o]) = bf16x4{p2a[0], p2a[1], p2b[0], p2b[1]};
+                *reinterpret_cast<bf16x4*>(&wsb[2][o]) = bf16x4{p3a[0], p3a[1], p3b[0], p3b[1]};
+            }
+        }
+    };
+    auto compute = [&](int k0) {
+        const int ksteps = min(BK / 32, (fin - k0 + 31) / 32);
+#pragma unroll
+        for (int s = 0; s < BK / 32; ++s) {
+            if (s < ksteps) {  // block-uniform
+                // A fragments of the wave's row groups split once; B fragments one
+                // column tile at a time, each feeding RG row groups
+                bf16x8 x1[RG], x2[RG], x3[RG];
+#pragma unroll
+                for (int g = 0; g < RG; ++g) {
+                    const float* xa = xsm + (w * 16 * RG + 16 * g + cl) * XS + 32 * s + 8 * kq;
+                    split3_x8(*reinterpret_cast<const f32x4*>(xa),
+                              *reinterpret_cast<const f32x4*>(xa + 4), x1[g], x2[g], x3[g]);
+                }
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const int o = (t * 16 + cl) * WSB + 32 * s + 8 * kq;
+                    const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&wsb[0][o]);
+                    const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&wsb[1][o]);
+                    const bf16x8 b3 = *reinterpret_cast<const bf16x8*>(&wsb[2][o]);
+#pragma unroll
+                    for (int g = 0; g < RG; ++g) {
+                        acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[g], b1, acc[g][t], 0, 0, 0);
+                        cor[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[g], b2, cor[g][t], 0, 0, 0);
+                        cor[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2[g], b1, cor[g][t], 0, 0, 0);
+                        cor[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[g], b3, cor[g][t], 0, 0, 0);
+                        cor[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2[g], b2, cor[g][t], 0, 0, 0);
+                        cor[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x3[g], b1, cor[g][t], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    };
+    // chunk c's loads were issued two chunks earlier.  Every load is
+    // unconditional (chunks past fin load the last chunk again, unused): a
+    // conditional load makes the compiler's vmcnt bookkeeping assume the worst
+    // at the join and wait for ALL loads in flight, the prefetch included.
+    const int klast = (fin - 1) / BK * BK;  // first k of the last chunk
+    // (sched_barrier: the two chunks' loads stay in issue order, so the oldest
+    // 16 are one chunk and the stage waits for that chunk alone)
+    load_chunk(0, xa_, wa_);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PD == 1) {  // one chunk in flight (fewer registers, more waves)
+        for (int k0 = 0; k0 < fin; k0 += BK) {
+            __syncthreads();
+            stage(k0, xa_, wa_);
+            __syncthreads();
+            load_chunk(min(k0 + BK, klast), xa_, wa_);
+            compute(k0);
+        }
+    } else {
+    load_chunk(min(BK, klast), xb_, wb_);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int k0 = 0; k0 < fin; k0 += 2 * BK) {
+        __syncthreads();  // the previous chunk's fragment reads are done
+        stage(k0, xa_, wa_);
+        __syncthreads();
+        load_chunk(min(k0 + 2 * BK, klast), xa_, wa_);
+        compute(k0);
+        __syncthreads();
+        stage(k0 + BK, xb_, wb_);  // past fin: zero W (ok is false), no k-steps
+        __syncthreads();
+        load_chunk(min(k0 + 3 * BK, klast), xb_, wb_);
+        compute(k0 + BK);
+    }
+    }
+    __syncthreads();  // x/W tiles dead: the x tile becomes the output tile
+#pragma unroll
+    for (int g = 0; g < RG; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[g][t] += cor[g][t];
+
+    const int hfp = round_up4(HF);
+    const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
+    float* Os = xsm;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int cc = t * 16 + cl;
+        const float bb = cc < HF ? bW[cc] : 0.f;
+        const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
+        const int h = cc >> lf, li = cl & (F - 1);
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+            float p1[4], p2[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = acc[g][t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
+                Os[(w * 16 * RG + 16 * g + kq * 4 + i) * OS + cc] = cc < HF ? v : 0.f;
+                p1[i] = group_sum16(v * w1, F);
+                p2[i] = group_sum16(v * w2, F);
+            }
+            // lane li (< 4) of the head's F lanes stores row kq*4 + li's sums
+            if (li < 4 && li < F && h < H) {
+                const float v1 = li == 0 ? p1[0] : li == 1 ? p1[1] : li == 2 ? p1[2] : p1[3];
+                const float v2 = li == 0 ? p2[0] : li == 1 ? p2[1] : li == 2 ? p2[2] : p2[3];
+                const int rr = row0 + 16 * g + kq * 4 + li;
+                if (rr < n) {
+                    if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = v1 + c1[h];
+                    s_dst[(size_t)rr * H + h] = v2 + c2[h];
+                }
+            }
+            if (F < 4 && li == 0 && h < H) {  // heads narrower than 4 lanes: rows F..3
+#pragma unroll
+                for (int i = 1; i < 4; ++i) {
+                    const int rr = row0 + 16 * g + kq * 4 + i;
+                    if (i >= F && rr < n) {
+                        if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
+                        s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    constexpr int C4 = NT * 4;
+    static_assert(NTH % C4 == 0, "NT must divide 16");
+    const int col = 4 * (tid % C4);
+    if (col < hfp) {
+        const int g = col / slice_w;
+        float* dst = Wh + (size_t)g * (size_t)slice_stride + (col - g * slice_w);
+        const int rows = min(BM, n - blk0);
+        for (int r = tid / C4; r < rows; r += NTH / C4)
+            *reinterpret_cast<f32x4*>(dst + (size_t)(blk0 + r) * ld_wh) =
+                *reinterpret_cast<const f32x4*>(Os + r * OS + col);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Projection, whole-K variant (fin <= 64): the workgroup's 64 X rows are one
 // contiguous 64*fin*4-byte chunk of HBM, and W [HF, fin] is contiguous too, so
 // both are staged into LDS with fully coalesced float4 loads (16x fewer
@@ -2114,7 +2385,8 @@ int status_of(hipError_t e) { return e == hipSuccess ? GAT_OK : (int)e; }
 const char* const kKnobNames[] = {
     "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_EDGE_LDS",  "GAT_EDGE_V",   "GAT_EDGE_U",
     "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
-    "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG"};
+    "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
+    "GAT_PROJ_BM"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -2234,10 +2506,31 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         const dim3 gp((n + 127) / 128), bp(256);
         const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
         const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
+        // split-bf16 matrix cores (k_project_x3) unless GAT_PROJ_X3=0 (A/B knob:
+        // the fp32-MFMA k_project_pipe2)
+        bool x3 = true;
+        if (const char* v = knob("GAT_PROJ_X3")) x3 = std::atoi(v) != 0;
+        // rows per block (GAT_PROJ_BM A/B knob: 64 = one 16-row group per wave,
+        // 128 = two, sharing every B fragment)
+        // tools/proj_ab.py: 4-float x rows (arxiv) prefer 64 rows per block with two
+        // chunks in flight, 2-float rows (Reddit's 602) 128 rows sharing B
+        // fragments with one chunk in flight
+        int bm = lw == 4 ? 64 : 128;
+        if (const char* v = knob("GAT_PROJ_BM")) bm = std::atoi(v);
 #define GAT_PIPE2(NT, LWV)                                                                     \
-    hipLaunchKernelGGL((k_project_pipe2<NT, LWV>), gp, bp, 0, st, x, n, fin, w, b, a_src,     \
-                       c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,      \
-                       slice_w, slice_stride)
+    if (x3 && bm == 128)                                                                       \
+        hipLaunchKernelGGL((k_project_x3<NT, LWV, 2, 1>), dim3((n + 127) / 128), bp, 0, st,    \
+                           x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,     \
+                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride);                 \
+    else if (x3)                                                                               \
+        hipLaunchKernelGGL((k_project_x3<NT, LWV, 1, 2>), dim3((n + 63) / 64), bp, 0, st, x, n, \
+                           fin, w, b, a_src,                                                  \
+                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
+                           slice_w, slice_stride);                                            \
+    else                                                                                       \
+        hipLaunchKernelGGL((k_project_pipe2<NT, LWV>), gp, bp, 0, st, x, n, fin, w, b, a_src, \
+                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
+                           slice_w, slice_stride)
 #define GAT_PIPE2_LW(NT)                                  \
     if (lw == 4) { GAT_PIPE2(NT, 4); }                    \
     else if (lw == 2) { GAT_PIPE2(NT, 2); }               \

@@ -31,7 +31,8 @@ VARIANTS = {
     "fast_u16": {"GAT_EDGE_U": "16"},
     "gather_score": {"GAT_EDGE_SCORE": "gather"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
-    "proj_pipe": {"GAT_PROJ_KERNEL": "pipe"},
+    "proj_pipe": {"GAT_PROJ_KERNEL": "pipe"},  # split-bf16 MFMA (k_project_x3)
+    "proj_pipe_fp32": {"GAT_PROJ_KERNEL": "pipe", "GAT_PROJ_X3": "0"},  # fp32 MFMA
     "v2": {"GAT_EDGE_V": "2"},
     "v4_natural": {"GAT_EDGE_V": "4", "GAT_EDGE_ORDER": "natural"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
@@ -52,7 +53,7 @@ VARIANTS = {
 def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
-              "GAT_HUB_SPLIT", "GAT_HUB_SEG"):
+              "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_X3"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)

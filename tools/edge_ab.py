@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of edge-kernel variants in the layer's own table layout
+(sliced planes where the layer uses them), in ONE process.  A variant is a set
+of GAT_* knobs, e.g. ``base`` (no knobs) or ``GAT_EDGE_R=2,GAT_EDGE_U=8``.
+Outputs are compared against the first variant (max |diff|).
+
+    python tools/edge_ab.py --workload reddit --rounds 5 \
+        --variants "base;GAT_EDGE_R=2,GAT_EDGE_U=8;GAT_EDGE_R=4,GAT_EDGE_U=8"
+
+``--only K`` runs variant K alone, ``--iters`` times, eagerly (for rocprofv3
+--pmc passes: every launch of the kernel is then that variant).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import torch  # noqa: E402
+
+from atmlgraphattentionnetworks_amd import tuning  # noqa: E402
+
+from tune_edge import time_fn  # noqa: E402
+
+KNOBS = ("GAT_EDGE_R", "GAT_EDGE_U", "GAT_EDGE_V", "GAT_EDGE_PIPE", "GAT_EDGE_LDS",
+         "GAT_WH_SLICES", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_ORDER", "GAT_PROJ_X3",
+         "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_PROJ_BM")
+
+
+def parse(spec):
+    """knobs of a variant; the pseudo-knob ``passes=W`` runs the edge work as W
+    source-window passes (gat_edge_aggregate_seg, online-softmax state carried
+    in memory between passes)."""
+    if spec in ("", "base"):
+        return {}
+    return dict(kv.split("=", 1) for kv in spec.split(","))
+
+
+def window_segments(csr, windows):
+    """[windows + 1, N] int32: pass c covers CSR positions [seg[c], seg[c+1]) of
+    each row, the in-edges whose source lies in window c of the node range."""
+    n = csr.num_nodes
+    rp = csr.rowptr.to(torch.int64)
+    deg = rp[1:] - rp[:-1]
+    row_id = torch.repeat_interleave(torch.arange(n, device=rp.device), deg)
+    blk = (n + windows - 1) // windows
+    ch = csr.col.to(torch.int64) // blk
+    cnt = torch.zeros(n * windows, dtype=torch.int64, device=rp.device)
+    cnt.index_add_(0, row_id * windows + ch, torch.ones_like(ch))
+    del row_id, ch
+    seg = torch.empty(windows + 1, n, dtype=torch.int32, device=rp.device)
+    seg[0] = rp[:-1].to(torch.int32)
+    seg[1:] = (rp[:-1].unsqueeze(1) + cnt.view(n, windows).cumsum(1)).t().to(torch.int32)
+    return seg
+
+
+def apply(env):
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    tuning.reload()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="reddit")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--variants", default="base")
+    ap.add_argument("--only", type=int, default=-1)
+    ap.add_argument("--layer", action="store_true", help="also time the whole layer forward")
+    args = ap.parse_args()
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
+    from atmlgraphattentionnetworks_amd.layer import ForwardPlan, gat_forward
+    from atmlgraphattentionnetworks_amd import _lib
+    from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
+
+    lib = _lib.load()
+    dev = torch.device("cuda", 0)
+    w = WORKLOADS[args.workload]
+    x, ei = make_inputs(w, dev)
+    n = x.size(0)
+    torch.manual_seed(0)
+    layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
+                                concat=w.concat).to(dev).eval()
+    csr = get_csr(ei, n)
+    del ei
+    pp = layer.packed()
+    bias = layer.bias.detach()
+    specs = [s.strip() for s in args.variants.split(";") if s.strip()]
+    envs = [parse(s) for s in specs]
+    knob_envs = [{k: v for k, v in e.items() if k != "passes"} for e in envs]
+
+    plan_out = {}
+    H, F = w.heads, w.out_channels
+    hf = H * F
+
+    class Passes:
+        """The edge work as W source-window passes over the plan's table."""
+
+        def __init__(self, plan, windows):
+            self.plan, self.windows = plan, windows
+            self.seg = window_segments(csr, windows)
+            self.st_acc = torch.empty(n, (hf + 3) // 4 * 4, device=dev)
+            self.st_ml = torch.empty(n, 2 * H, device=dev)
+
+        def edge(self, lib, csr_, pp_, bias_, out):
+            p = self.plan
+            stream = torch._C._cuda_getCurrentRawStream(dev.index)
+            ld = hf // p.slices if p.slices > 1 else p.hfp
+            for c in range(self.windows):
+                flags = (_lib.GAT_SEG_LOAD if c > 0 else 0) | \
+                    (_lib.GAT_SEG_STORE if c < self.windows - 1 else 0)
+                rc = lib.gat_edge_aggregate_seg(
+                    self.seg[c].data_ptr(), self.seg[c + 1].data_ptr(), 0, csr.col.data_ptr(),
+                    csr.order.data_ptr(), 0, n, p.p_wh, ld, n, p.slices, pp.a_src.data_ptr(),
+                    pp.c_src.data_ptr(), p.p_sd, H, F, 1, 0.2, self.st_acc.data_ptr(),
+                    self.st_ml.data_ptr(), flags, 0, bias.data_ptr(), out.data_ptr(), p.hint,
+                    stream)
+                _lib.check(rc, "seg pass")
+            return out
+
+        def kernel_name(self):
+            return f"{self.windows} source-window passes: " + self.plan.kernel_name()
+
+    def plan_for(env):
+        env = dict(env)
+        windows = int(env.pop("passes", "0"))
+        apply(env)
+        plan = ForwardPlan(x, csr, w.heads, w.out_channels, w.concat, 0.2)
+        plan.project(lib, x, pp)
+        if windows > 1:
+            plan = Passes(plan, windows)
+        plan_out[id(plan)] = torch.empty(n, hf if w.concat else F, device=dev)
+        return plan
+
+    with torch.no_grad():
+        if args.only >= 0:
+            plan = plan_for(envs[args.only])
+            apply(knob_envs[args.only])
+            for _ in range(args.iters):
+                plan.edge(lib, csr, pp, bias, plan_out[id(plan)])
+            torch.cuda.synchronize()
+            print(json.dumps({"variant": specs[args.only], "kernel": plan.kernel_name()}))
+            return
+        plans = [plan_for(e) for e in envs]
+        res = {s: [] for s in specs}
+        lres = {s: [] for s in specs}
+        outs = {}
+        for _ in range(args.rounds):
+            for s, env, plan in zip(specs, knob_envs, plans):
+                apply(env)
+                o = plan_out[id(plan)]
+                res[s].append(time_fn(lambda: plan.edge(lib, csr, pp, bias, o), args.iters))
+                outs[s] = o.clone()
+                if args.layer:
+                    lres[s].append(time_fn(
+                        lambda: gat_forward(x, csr, pp, bias, w.heads, w.out_channels, w.concat,
+                                            0.2), args.iters))
+        apply({})
+    ref = outs[specs[0]]
+    summary = {}
+    for s in specs:
+        med = statistics.median(res[s])
+        d = {"edge_median_ms": round(med, 5), "edge_min_ms": round(min(res[s]), 5),
+             "edges_per_s": csr.num_edges / med * 1e3,
+             "max_abs_diff_vs_first": float((outs[s] - ref).abs().max()),
+             "kernel": plans[specs.index(s)].kernel_name()}
+        if args.layer:
+            d["layer_median_ms"] = round(statistics.median(lres[s]), 5)
+        summary[s] = d
+    print(json.dumps({"workload": args.workload, "N": n, "E'": csr.num_edges,
+                      "max_abs_ref": float(ref.abs().max()), "results": summary}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
