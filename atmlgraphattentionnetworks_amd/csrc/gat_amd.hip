@@ -36,6 +36,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <type_traits>
 
@@ -800,6 +801,180 @@ __global__ __launch_bounds__(256) void k_project_x3(
         for (int r = tid / C4; r < rows; r += NTH / C4)
             *reinterpret_cast<f32x4*>(dst + (size_t)(blk0 + r) * ld_wh) =
                 *reinterpret_cast<const f32x4*>(Os + r * OS + col);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Projection for Fin <= 128 (PPI's 50, ogbn-arxiv's 128): W resident in LDS,
+// x streamed straight into MFMA fragments.
+//
+// With the whole K range small, W [HF, Fin] split into its three bf16 planes
+// (k_project_x3's exact split) fits in LDS (arxiv: 3 x 64 x 136 bf16 = 52 KB),
+// so each workgroup splits W ONCE and its waves then loop over 16-row tiles of
+// x independently: no per-chunk W reloads or splits (with 64-row blocks W
+// cost as many loads as x at arxiv), no x staging through LDS and no
+// workgroup barriers in the loop.  Lane l loads its A fragments
+// x[row l&15][k 8(l>>4)..+8] directly (each x byte read once; a row's 4 lanes
+// x 2 loads fill its 128-B lines), splits them as soon as they land, and
+// issues the next tile's loads before this tile's MFMAs, so a tile's loads
+// are in flight during the previous tile's MFMAs and epilogue.  The epilogue
+// (bias, fused scores by DPP, Wh rows through a per-wave LDS tile for
+// coalesced float4 stores, row-major or column planes) is k_project_x3's.
+// ---------------------------------------------------------------------------
+template <int NT, int LW, int KS>
+__global__ __launch_bounds__(256, 2) void k_project_wres(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
+    float* __restrict__ s_dst, int slice_w, long long slice_stride) {
+    constexpr int BN = NT * 16, KP = KS * 32;  // padded K
+    constexpr int WSB = KP + 8, OS = BN + 4;
+    constexpr int NL = 8 / LW;                  // loads per 8-float fragment
+    using vec = typename std::conditional<LW == 4, f32x4,
+                typename std::conditional<LW == 2, f32x2, float>::type>::type;
+    __shared__ __attribute__((aligned(16))) __bf16 wsb[3][BN * WSB];
+    __shared__ __attribute__((aligned(16))) float osm[4][16 * OS];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    // W split into three bf16 planes, zero past HF columns and past fin
+    for (int e = 2 * tid; e < BN * KP; e += 2 * 256) {
+        const int c = e / KP, k = e % KP;  // k even, KP even: the pair shares a row
+        const bool ok = c < HF;
+        const float v0 = ok && k < fin ? W[(size_t)c * fin + k] : 0.f;
+        const float v1 = ok && k + 1 < fin ? W[(size_t)c * fin + k + 1] : 0.f;
+        bf16x2 p1, p2, p3;
+        split3_pair(f32x2{v0, v1}, p1, p2, p3);
+        const int o = c * WSB + k;
+        *reinterpret_cast<bf16x2*>(&wsb[0][o]) = p1;
+        *reinterpret_cast<bf16x2*>(&wsb[1][o]) = p2;
+        *reinterpret_cast<bf16x2*>(&wsb[2][o]) = p3;
+    }
+    __syncthreads();
+
+    const int hfp = round_up4(HF);
+    const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
+    float bb[NT], w1[NT], w2[NT];
+    // (and c1/c2 per head: epilogue parameters stay in registers, since a global
+    // load inside the tile loop would wait, vmcnt being in order, for the next
+    // tile's x loads in flight)
+    float cs1[NT], cs2[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int cc = t * 16 + cl;
+        bb[t] = cc < HF ? bW[cc] : 0.f;
+        w1[t] = cc < HF ? a1[cc] : 0.f;
+        w2[t] = cc < HF ? a2[cc] : 0.f;
+        const int h = min(cc >> lf, H - 1);
+        cs1[t] = c1[h];
+        cs2[t] = c2[h];
+    }
+    float* Os = osm[w];
+    const int tiles = (n + 15) / 16;
+    const int tstride = gridDim.x * 4;
+    int tile = blockIdx.x * 4 + w;
+    // x fragments of one tile: KS k-steps x NL loads (rows past n clamp to n-1,
+    // k past fin to fin-LW: in bounds, and they meet zero W)
+    vec xr[KS][NL];
+    auto load_tile = [&](int tl) {
+        const int r = min(tl * 16 + cl, n - 1);
+        const float* xrow = X + (size_t)r * fin;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int q = 0; q < NL; ++q) {
+                const int k = min(32 * s + 8 * kq + LW * q, fin - LW);
+                xr[s][q] = *reinterpret_cast<const vec*>(xrow + k);
+            }
+    };
+    load_tile(min(tile, tiles - 1));
+    for (; tile < tiles; tile += tstride) {
+        // split this tile's fragments (frees xr), then start the next tile's loads
+        bf16x8 x1[KS], x2[KS], x3[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            float f[8];
+#pragma unroll
+            for (int q = 0; q < NL; ++q)
+#pragma unroll
+                for (int j = 0; j < LW; ++j) {
+                    if constexpr (LW == 1) f[q] = xr[s][q];
+                    else f[q * LW + j] = xr[s][q][j];
+                }
+            split3_x8(f32x4{f[0], f[1], f[2], f[3]}, f32x4{f[4], f[5], f[6], f[7]}, x1[s],
+                      x2[s], x3[s]);
+        }
+        // unconditional (the last tile re-loads itself, unused): a conditional
+        // load would make the compiler wait for every older store at the loop top
+        load_tile(min(tile + tstride, tiles - 1));
+        f32x4 acc[NT], cor[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = cor[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int o = (t * 16 + cl) * WSB + 32 * s + 8 * kq;
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&wsb[0][o]);
+                const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&wsb[1][o]);
+                const bf16x8 b3 = *reinterpret_cast<const bf16x8*>(&wsb[2][o]);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[s], b1, acc[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[s], b2, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2[s], b1, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1[s], b3, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2[s], b2, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x3[s], b1, cor[t], 0, 0, 0);
+            }
+        }
+        const int row0 = tile * 16;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int cc = t * 16 + cl;
+            const int h = cc >> lf, li = cl & (F - 1);
+            float p1[4], p2[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = acc[t][i] + cor[t][i] + bb[t];  // Linear bias (GAT.py:43)
+                Os[(kq * 4 + i) * OS + cc] = cc < HF ? v : 0.f;
+                p1[i] = group_sum16(v * w1[t], F);
+                p2[i] = group_sum16(v * w2[t], F);
+            }
+            if (li < 4 && li < F && h < H) {
+                const float v1 = li == 0 ? p1[0] : li == 1 ? p1[1] : li == 2 ? p1[2] : p1[3];
+                const float v2 = li == 0 ? p2[0] : li == 1 ? p2[1] : li == 2 ? p2[2] : p2[3];
+                const int rr = row0 + kq * 4 + li;
+                if (rr < n) {
+                    if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = v1 + cs1[t];
+                    s_dst[(size_t)rr * H + h] = v2 + cs2[t];
+                }
+            }
+            if (F < 4 && li == 0 && h < H) {  // heads narrower than 4 lanes: rows F..3
+#pragma unroll
+                for (int i = 1; i < 4; ++i) {
+                    const int rr = row0 + kq * 4 + i;
+                    if (i >= F && rr < n) {
+                        if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + cs1[t];
+                        s_dst[(size_t)rr * H + h] = p2[i] + cs2[t];
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // Wh rows of the tile: float4 columns, 16 rows (row-major or planes)
+        constexpr int C4 = BN / 4;
+#pragma unroll
+        for (int idx = lane; idx < 16 * C4; idx += 64) {
+            const int r = idx / C4, col = 4 * (idx % C4);
+            if (col < hfp && row0 + r < n) {
+                const int g = col / slice_w;
+                *reinterpret_cast<f32x4*>(Wh + (size_t)g * (size_t)slice_stride +
+                                          (size_t)(row0 + r) * ld_wh + (col - g * slice_w)) =
+                    *reinterpret_cast<const f32x4*>(Os + r * OS + col);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -2386,7 +2561,7 @@ const char* const kKnobNames[] = {
     "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_EDGE_LDS",  "GAT_EDGE_V",   "GAT_EDGE_U",
     "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
     "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
-    "GAT_PROJ_BM"};
+    "GAT_PROJ_BM",     "GAT_PROJ_WRES"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -2475,6 +2650,42 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     const size_t wk_lds = (size_t)wk_lds_floats(fin, nt) * sizeof(float);
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) |
                              reinterpret_cast<uintptr_t>(wh)) & 15) == 0;
+    // W-resident kernel for 64 < fin <= 128 (k_project_wres: arxiv 44.4 -> 38.4 us
+    // against k_project_x3; at PPI's fin 50 the whole-K fp32 k_project_wk stays
+    // faster, 10.4 vs 12.5 us: 1.4 tiles per wave do not amortise the W split).
+    // GAT_PROJ_WRES (A/B knob): 0 never, 1 for every fin <= 128.
+    bool wres = fin > 64;
+    if (const char* v = knob("GAT_PROJ_WRES")) wres = std::atoi(v) != 0;
+    if (pk != nullptr && std::strcmp(pk, "wres") != 0) wres = false;
+    if (wres && fin > 0 && fin <= 128 && (nt == 1 || nt == 2 || nt == 4) && pow2_f && f <= 16) {
+        const uintptr_t xa = reinterpret_cast<uintptr_t>(x);
+        const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
+        const int ks = fin <= 32 ? 1 : fin <= 64 ? 2 : 4;
+        const long long tiles = (n + 15) / 16;
+        // persistent beyond two workgroups per CU (each wave loops over tiles)
+        const int grid_w = (int)std::min<long long>((tiles + 3) / 4, 256 * 2);
+#define GAT_WRES(NTV, LWV, KSV)                                                               \
+    hipLaunchKernelGGL((k_project_wres<NTV, LWV, KSV>), dim3(grid_w), dim3(256), 0, st, x, n, \
+                       fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src,  \
+                       ld_s, s_dst, slice_w, slice_stride)
+#define GAT_WRES_KS(NTV, LWV)                                          \
+    switch (ks) {                                                      \
+        case 1: GAT_WRES(NTV, LWV, 1); break;                          \
+        case 2: GAT_WRES(NTV, LWV, 2); break;                          \
+        default: GAT_WRES(NTV, LWV, 4); break;                         \
+    }
+#define GAT_WRES_LW(NTV)                                               \
+    if (lw == 4) { GAT_WRES_KS(NTV, 4) }                               \
+    else if (lw == 2) { GAT_WRES_KS(NTV, 2) }                          \
+    else { GAT_WRES_KS(NTV, 1) }
+        if (nt == 1) { GAT_WRES_LW(1) }
+        else if (nt == 2) { GAT_WRES_LW(2) }
+        else { GAT_WRES_LW(4) }
+#undef GAT_WRES_LW
+#undef GAT_WRES_KS
+#undef GAT_WRES
+        return status_of(hipGetLastError());
+    }
     int wk_max = 64;  // GAT_PROJ_WK_MAX (A/B knob): largest fin for the whole-K kernel
     if (const char* v = knob("GAT_PROJ_WK_MAX")) wk_max = std::atoi(v);
     const bool wk_ok = fin > 0 && fin <= wk_max && aligned16 && wk_lds <= 160 * 1024 &&

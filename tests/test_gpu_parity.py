@@ -26,6 +26,8 @@ def dev():
 # shape allows) AND on the generic kernels, selected by the library's env knobs.
 VARIANTS = {
     "fast": {},
+    "proj_wk": {"GAT_PROJ_WRES": "0"},  # whole-K fp32 / K-chunked projections
+    "proj_wres": {"GAT_PROJ_WRES": "1"},  # W-resident split-bf16 for every fin <= 128
     "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds"},
     "fast_u4": {"GAT_EDGE_U": "4"},
     "fast_u16": {"GAT_EDGE_U": "16"},
@@ -53,7 +55,8 @@ VARIANTS = {
 def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
-              "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_X3"):
+              "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_X3", "GAT_PROJ_WRES",
+              "GAT_PROJ_BM"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -120,6 +123,9 @@ CASES = [
     (300, 3000, 129, 3, 8, True, "uniform"),  # HF = 24: a half-used tile
     (300, 3000, 200, 1, 16, True, "uniform"),  # one 16-wide head
     (257, 3000, 128, 8, 8, True, "uniform"),  # rows not a multiple of the 128-row block
+    # k_project_wres (64 < Fin <= 128): partial 16-row tiles, NT = 1 / 4
+    (333, 4000, 100, 8, 8, True, "uniform"),
+    (50, 500, 66, 4, 4, False, "uniform"),
     (700, 9000, 0, 3, 4, True, "uniform"),  # Fin = 0: Wh = bias
 ]
 
