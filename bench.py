@@ -41,6 +41,40 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md: ~34.5 TB/s)
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (v_mfma_f32_16x16x4_f32)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 matrix peak (v_mfma_f32_16x16x32_bf16)
+SPLIT_PRODUCTS = 6  # bf16 MFMA products per fp32 product in the split-bf16 projections
+
+
+def projection_kernel(fin: int) -> dict:
+    """The projection kernel the library picks for this Fin (gat_amd.hip
+    project_impl, default knobs) and the matrix dtype it issues."""
+    if fin <= 64:
+        return {"kernel": "k_project_wk", "mfma": "fp32 (v_mfma_f32_16x16x4_f32)",
+                "split": False}
+    name = "k_project_wres" if fin <= 128 else "k_project_x3"
+    return {"kernel": name, "mfma": "bf16, operands split exactly into 3 bf16 terms, "
+            "6 v_mfma_f32_16x16x32_bf16 per fp32 product", "split": True}
+
+
+def projection_roofline(flops: float, nbytes: float, ms: float, fin: int) -> dict:
+    """fp32-equivalent TFLOP/s, the fraction of the matrix peak of the dtype the
+    kernel issues, and the HBM fraction; ``bound`` = the larger of the two time
+    bounds."""
+    k = projection_kernel(fin)
+    sec = ms * 1e-3
+    if k["split"]:
+        mfma_flops, peak = SPLIT_PRODUCTS * flops, MFMA_BF16_PEAK_TFLOPS
+    else:
+        mfma_flops, peak = flops, MFMA_F32_PEAK_TFLOPS
+    t_mfma = mfma_flops / (peak * 1e12)
+    t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
+    return {"kernel": k["kernel"], "mfma_dtype": k["mfma"],
+            "TFLOPs": flops / sec / 1e12,
+            "mfma_issued_TFLOPs": mfma_flops / sec / 1e12, "mfma_peak_TFLOPs": peak,
+            "mfma_frac": mfma_flops / sec / 1e12 / peak,
+            "hbm_bytes": nbytes, "hbm_frac": nbytes / sec / 1e9 / HBM_PEAK_GBS,
+            "bound": "mfma" if t_mfma >= t_hbm else "hbm",
+            "bound_frac": max(t_mfma, t_hbm) / sec}
 NUM_CUS = 256
 METRIC = "edges/sec through 8-head GAT layer forward, PPI shape, at 1/2/4/8 MI355X"
 NORTH_STAR_REDDIT_EDGES_PER_S = 16.4e9  # SURVEY.md §8d: >= 60% of the §8d HBM ceiling
@@ -267,13 +301,8 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
             "effective_gather_GBps": alg / es / 1e9,
             "hub_rows_split": 0 if csr.hubs is None else csr.hubs.n_hub,
         },
-        "projection": {
-            "ms": proj_ms, "TFLOPs": flops / (proj_ms * 1e-3) / 1e12,
-            "mfma_frac": flops / (proj_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFLOPS,
-            "hbm_bytes": projection_bytes(n, w.in_channels, hf, w.heads),
-            "hbm_frac": projection_bytes(n, w.in_channels, hf, w.heads) / (proj_ms * 1e-3)
-            / 1e9 / HBM_PEAK_GBS,
-        },
+        "projection": dict(ms=proj_ms, **projection_roofline(
+            flops, projection_bytes(n, w.in_channels, hf, w.heads), proj_ms, w.in_channels)),
         "_inputs": (x, ei, layer),
     }
     _log(f"{name}: {res['value'] / 1e9:.2f} G edges/s, edge {edge_ms * 1e3:.1f} us, "
@@ -614,8 +643,10 @@ def main():
         "roofline": head_sum["roofline"],
         "breakdown_ms": {"project": head["projection"]["ms"], "edge": head["edge_kernel"]["ms"],
                          "csr_build_once": head["csr_build_once_ms"]},
-        "projection": {"bound": "mfma", "achieved": head["projection"]["TFLOPs"],
-                       "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "projection": {"bound": "mfma", "kernel": head["projection"]["kernel"],
+                       "mfma_dtype": head["projection"]["mfma_dtype"],
+                       "achieved": head["projection"]["mfma_issued_TFLOPs"],
+                       "peak": head["projection"]["mfma_peak_TFLOPs"], "unit": "TFLOP/s",
                        "frac": head["projection"]["mfma_frac"],
                        "mfma_busy_frac_pmc": head_sum["projection"].get("mfma_busy_frac_pmc"),
                        "hbm_frac": head["projection"]["hbm_frac"]},
