@@ -117,7 +117,8 @@ CASES = [
     (64, 0, 5, 4, 8, True, "uniform"),  # self-loops only
     (1, 0, 3, 2, 2, True, "uniform"),  # a single node
     (700, 9000, 602, 8, 8, True, "uniform"),  # Reddit's Fin
-    # k_project_pipe (Fin > 64): K tails and partial column tiles
+    # the K-chunked projections (Fin > 128; Fin > 64 with GAT_PROJ_WRES=0): K tails and
+    # partial column tiles
     (400, 5000, 65, 4, 8, True, "uniform"),  # one-column tail chunk, NT = 2
     (400, 5000, 130, 2, 4, False, "uniform"),  # HF = 8, NT = 1
     (300, 3000, 129, 3, 8, True, "uniform"),  # HF = 24: a half-used tile
