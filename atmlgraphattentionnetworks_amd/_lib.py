@@ -18,6 +18,7 @@ GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
 GAT_ABI_VERSION = 4
+GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
 GAT_SEG_LOAD = 1
 GAT_SEG_STORE = 2
 GAT_MAX_HEADS = 64

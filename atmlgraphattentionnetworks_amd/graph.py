@@ -45,6 +45,13 @@ class CSRGraph(NamedTuple):
     num_edges: int  # E + N (edges after add_self_loops)
     order: Optional[torch.Tensor] = None  # int32 [N], rows by descending in-degree
     hubs: Optional[HubPlan] = None  # split schedule for rows far above the average
+    local: bool = False  # sources lie near their targets in node order (locality_hint)
+
+    def kernel_hint(self) -> int:
+        """The edge kernels' scheduling hint: E'/N, with GAT_HINT_LOCAL OR'd in
+        for a local graph (include/gat_amd.h)."""
+        h = self.num_edges // max(self.num_nodes, 1)
+        return h | _lib.GAT_HINT_LOCAL if self.local and h > 0 else h
 
 
 def _check_edge_index(edge_index: torch.Tensor, device: torch.device) -> torch.Tensor:
@@ -85,7 +92,26 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int,
         # PyG's index_select raises on the same input (GAT.py:53 -> __lift__)
         raise ValueError(f"edge_index contains node ids outside [0, {num_nodes})")
     return CSRGraph(rowptr, col, num_nodes, E + num_nodes, order,
-                    hub_plan(rowptr, order, E + num_nodes))
+                    hub_plan(rowptr, order, E + num_nodes), locality_hint(rowptr, col, num_nodes))
+
+
+def locality_hint(rowptr: torch.Tensor, col: torch.Tensor, num_nodes: int,
+                  window: int = 1024, samples: int = 65536) -> bool:
+    """Whether most edges join nodes within ``window`` of each other in node
+    order (block-diagonal batches of small graphs such as the CIFAR10
+    superpixel batches, kNN graphs): then the rows a wave processes together
+    share source rows, and narrow rows prefer two float4s per lane
+    (GAT_HINT_LOCAL).  Judged on up to ``samples`` evenly spaced CSR entries;
+    graphs of at most 4 * window nodes are never called local (every edge
+    would be)."""
+    nnz = col.numel()
+    if nnz == 0 or num_nodes <= 4 * window:
+        return False
+    k = min(nnz, samples)
+    pos = torch.linspace(0, nnz - 1, k, device=col.device).to(torch.int64)
+    row = torch.searchsorted(rowptr[1:].to(torch.int64), pos, right=True)
+    near = ((col[pos].to(torch.int64) - row).abs() <= window).to(torch.float32).mean()
+    return bool(near >= 0.5)
 
 
 def hub_segment_len(num_edges: int) -> int:

@@ -201,7 +201,8 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
     order = getattr(csr, "order", None)
     if order is not None and tuning.get("GAT_EDGE_ORDER") == "natural":  # A/B knob
         order = None
-    hint = csr.num_edges // max(csr.num_nodes, 1)
+    hint = csr.kernel_hint() if hasattr(csr, "kernel_hint") else \
+        csr.num_edges // max(csr.num_nodes, 1)
     if table.slices > 1:
         if pp is None or lse is not None:
             raise ValueError("the sliced edge kernel recomputes s_src (pp) and has no lse")
@@ -279,7 +280,8 @@ def _edge_hubs(lib, csr: CSRGraph, wh_ptr: int, ld_wh: int, n_table: int, slices
     p_acc = st.data_ptr()
     p_ml = p_acc + 4 * nv * hf4
     n_pos = hubs.sched_row.numel()
-    hint = csr.num_edges // max(csr.num_nodes, 1)
+    hint = csr.kernel_hint() if hasattr(csr, "kernel_hint") else \
+        csr.num_edges // max(csr.num_nodes, 1)
     rc = lib.gat_edge_aggregate_seg(
         hubs.sched_b.data_ptr(), hubs.sched_e.data_ptr(), 1, csr.col.data_ptr(),
         hubs.sched_row.data_ptr(), 0, n_pos, wh_ptr, ld_wh, n_table, slices,
@@ -301,7 +303,7 @@ class ForwardPlan:
     two phases of exactly the path the layer runs."""
 
     __slots__ = ("n", "fin", "heads", "f", "hf", "hfp", "concat", "slope", "slices", "split",
-                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint")
+                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint")
 
     def __init__(self, x: torch.Tensor, csr: CSRGraph, heads: int, f: int, concat: bool,
                  negative_slope: float):
@@ -317,6 +319,8 @@ class ForwardPlan:
         self.dev = x.device.index
         self.hint = csr.num_edges // max(n, 1)
         self.slices = wh_slices(heads, f, concat, negative_slope, self.hint)
+        # the kernels' hint: + GAT_HINT_LOCAL for a local graph (CSRGraph.kernel_hint)
+        self.khint = csr.kernel_hint() if hasattr(csr, "kernel_hint") else self.hint
         self.split = csr.hubs is not None and fused_score_ok(heads, f, negative_slope)
 
     def project(self, lib, x: torch.Tensor, pp: PackedParams) -> None:
@@ -356,14 +360,14 @@ class ForwardPlan:
             rc = lib.gat_edge_aggregate_sliced(
                 csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, self.p_wh, n,
                 self.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
-                self.slope, bias.data_ptr(), out.data_ptr(), self.hint, stream)
+                self.slope, bias.data_ptr(), out.data_ptr(), self.khint, stream)
             if rc:
                 _lib.check(rc, "gat_edge_aggregate_sliced")
             return out
         rc = lib.gat_edge_aggregate(
             csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, self.p_wh, self.hfp,
             self.p_ss, heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
-            int(self.concat), self.slope, bias.data_ptr(), out.data_ptr(), 0, self.hint, stream)
+            int(self.concat), self.slope, bias.data_ptr(), out.data_ptr(), 0, self.khint, stream)
         if rc:
             _lib.check(rc, "gat_edge_aggregate")
         return out

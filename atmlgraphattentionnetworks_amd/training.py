@@ -104,7 +104,7 @@ class GATFunction(torch.autograd.Function):
             0, n, wh.data_ptr(), hfp, s_src.data_ptr(), heads, pp.a_src.data_ptr(),
             pp.c_src.data_ptr(), s_dst.data_ptr(), heads, f, int(concat), act, act_param, p,
             seed, p_seed, bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(),
-            csr.num_edges // max(n, 1), stream)
+            csr.kernel_hint(), stream)
         if rc:
             _lib.check(rc, "gat_edge_aggregate_ex")
         ctx.save_for_backward(x, ws)
@@ -189,7 +189,7 @@ def _backward_recompute(ctx, g, ws, csc, stream):
     bw = torch.empty(o_ps + pw + sws, dtype=torch.float32, device=g.device)
     base = bw.data_ptr()
     order = csr.order
-    hint = csr.num_edges // max(n, 1)
+    hint = csr.kernel_hint()
     rc = lib.gat_bwd_targets(
         csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(), 0,
         n, p_wh, hfp, pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, p_lse, p_y, g.data_ptr(),

@@ -113,10 +113,16 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
  *   lse          optional [rows, heads] = max + log(sum exp) per (row, head)
  *                (natural log; for the backward pass); may be NULL
  *   edges_per_row_hint  average in-degree (E'/rows) or 0 if unknown: picks the
- *                edge-chunk length, never affects results
+ *                edge-chunk length, never affects results; GAT_HINT_LOCAL may be
+ *                OR'd in (every entry point taking a hint accepts it)
  * GAT_EUNSUPPORTED if s_src is NULL and the shape needs it (f % 4 != 0, or
  * f/4 not a power of two, or negative_slope outside [0, 1]).
  */
+/* Scheduling hint bit: the graph's sources lie near their targets in node order
+ * (block-diagonal batches of small graphs, kNN graphs), so rows processed
+ * together share source rows.  Never affects results. */
+#define GAT_HINT_LOCAL (1 << 30)
+
 int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, int row_begin,
                        int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
                        const float* a_src, const float* c_src, const float* s_dst, int heads,
