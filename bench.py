@@ -40,6 +40,9 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md: ~34.5 TB/s)
+# measured chip-wide rate of row gathers served by the XCD's L2 (MI355X_MICROARCH.md,
+# "Indexed rows: gather into LDS": 16.8-18.8 TB/s); the edge kernel's practical ceiling
+L2_GATHER_CEILING_GBS = 18800.0
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (v_mfma_f32_16x16x4_f32)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 matrix peak (v_mfma_f32_16x16x32_bf16)
 SPLIT_PRODUCTS = 6  # bf16 MFMA products per fp32 product in the split-bf16 projections
@@ -458,7 +461,13 @@ def _roofline(meas: dict, traffic: dict) -> dict:
                        "(L2->fabric bytes; Infinity-Cache hits included, so an upper bound "
                        "on HBM bytes)"},
          "l2": {"request_bytes_per_launch": ek["l2_request_bytes"], "GBps": ek["l2_GBps"],
-                "peak": L2_PEAK_GBS, "frac": ek["l2_frac"]},
+                "peak": L2_PEAK_GBS, "frac": ek["l2_frac"],
+                "gather_ceiling_GBps": L2_GATHER_CEILING_GBS,
+                "frac_of_gather_ceiling": ek["l2_GBps"] / L2_GATHER_CEILING_GBS,
+                "what": "the kernel's L2 request rate (both 128-B plane rows, or the 256-B "
+                        "row, per edge) against the L2 spec and against the measured rate of "
+                        "L2-served row gathers, the practical ceiling of a gather kernel whose "
+                        "table stays on-die"},
          "effective_gather_GBps": ek["effective_gather_GBps"]}
     return r
 
