@@ -7,6 +7,7 @@ raises.  The symbols bound here are exactly the ones the header declares.
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
 import threading
 
@@ -140,6 +141,7 @@ def check(status: int, what: str) -> None:
         raise GatLibraryError(f"{what} failed: {msg}")
 
 
+@functools.lru_cache(maxsize=None)  # pure function of the shape
 def table_layout(heads: int, f: int):
     ld, s_off = ctypes.c_int(), ctypes.c_int()
     check(load().gat_table_layout(heads, f, ctypes.byref(ld), ctypes.byref(s_off)),
@@ -161,6 +163,7 @@ def csc_workspace_size(nnz: int, num_nodes: int) -> int:
     return out.value
 
 
+@functools.lru_cache(maxsize=None)  # pure function of the shape
 def weight_grad_workspace_size(num_nodes: int, fin: int, hf: int) -> int:
     out = ctypes.c_size_t()
     check(load().gat_weight_grad_workspace_size(num_nodes, fin, hf, ctypes.byref(out)),
@@ -168,6 +171,7 @@ def weight_grad_workspace_size(num_nodes: int, fin: int, hf: int) -> int:
     return out.value
 
 
+@functools.lru_cache(maxsize=None)  # pure function of the shape
 def bwd_table_layout(heads: int, f: int, concat: bool) -> int:
     ld = ctypes.c_int()
     check(load().gat_bwd_table_layout(heads, f, int(concat), ctypes.byref(ld)),
@@ -175,6 +179,7 @@ def bwd_table_layout(heads: int, f: int, concat: bool) -> int:
     return ld.value
 
 
+@functools.lru_cache(maxsize=None)  # pure function of the shape
 def bwd_sources_parts(num_nodes: int, heads: int, f: int) -> int:
     out = ctypes.c_int()
     check(load().gat_bwd_sources_parts(num_nodes, heads, f, ctypes.byref(out)),

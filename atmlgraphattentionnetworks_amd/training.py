@@ -151,6 +151,11 @@ class GATFunction(torch.autograd.Function):
         return (dx, dbias, None, None, None, None, *grads)
 
 
+def _line_up(floats: int) -> int:
+    """``floats`` rounded up to a whole 128-B line (32 floats)."""
+    return (floats + 31) // 32 * 32
+
+
 def _seed_ptr(ctx) -> int:
     return 0 if ctx.seed_slot is None else ctx.seed_slot.data_ptr()
 
@@ -181,9 +186,11 @@ def _backward_recompute(ctx, g, ws, csc, stream):
     parts = _lib.bwd_sources_parts(n, heads, f)
     sws = (parts + 255) // 256 * pw if parts > 256 else 0
     hfp, p_wh, p_ss, p_sd, p_lse, p_y = _saved_layout(ctx, ws)
-    # one workspace: ds_dst | target table | dwh | partials | sums | scratch
-    o_t = (n * heads + 3) // 4 * 4
-    o_dwh = o_t + n * ld_t
+    # one workspace: ds_dst | target table | dwh | partials | sums | scratch; the
+    # table starts on a 128-B line (its rows are whole lines: a row gathered per
+    # out-edge in pass 2 then touches 3 lines, not 4), and so does dwh
+    o_t = _line_up(n * heads)
+    o_dwh = _line_up(o_t + n * ld_t)
     o_part = o_dwh + n * hf
     o_ps = o_part + parts * pw
     bw = torch.empty(o_ps + pw + sws, dtype=torch.float32, device=g.device)
@@ -229,7 +236,7 @@ def _backward_stored(ctx, g, ws, csc, stream):
     hfp, p_wh, p_ss, p_sd, p_lse, p_y = _saved_layout(ctx, ws)
     # one workspace: ds_dst | (A, dz) per edge and head | dwh | partials | sums | scratch
     m = 2 * max(nnz, 1) * heads
-    o_dwh = n * heads + m
+    o_dwh = _line_up(n * heads + m)
     o_part = o_dwh + n * hf
     o_ps = o_part + parts * pw
     bw = torch.empty(o_ps + pw + sws, dtype=torch.float32, device=g.device)

@@ -490,10 +490,12 @@ def train_step(layer, x, ei, n_edges: int, steps: int) -> dict:
     xg = x.detach().clone().requires_grad_(True)
     gout = torch.randn(x.size(0), layer.num_heads * layer.output_channels if layer.concat
                        else layer.output_channels, device=x.device)
+    # gradients cleared as the reference's loops do (optimizer.zero_grad(),
+    # run_inductive.py:76); Module.zero_grad walks the module tree instead
+    opt = torch.optim.Adam([xg, *layer.parameters()], lr=1e-3)
 
     def one():
-        layer.zero_grad(set_to_none=True)
-        xg.grad = None
+        opt.zero_grad(set_to_none=True)
         layer(xg, ei).backward(gout)
 
     for _ in range(5):
