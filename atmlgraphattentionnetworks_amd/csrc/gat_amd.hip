@@ -839,18 +839,69 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int cl = lane & 15, kq = lane >> 4;
-    // W split into three bf16 planes, zero past HF columns and past fin
-    for (int e = 2 * tid; e < BN * KP; e += 2 * 256) {
-        const int c = e / KP, k = e % KP;  // k even, KP even: the pair shares a row
-        const bool ok = c < HF;
-        const float v0 = ok && k < fin ? W[(size_t)c * fin + k] : 0.f;
-        const float v1 = ok && k + 1 < fin ? W[(size_t)c * fin + k + 1] : 0.f;
-        bf16x2 p1, p2, p3;
-        split3_pair(f32x2{v0, v1}, p1, p2, p3);
-        const int o = c * WSB + k;
-        *reinterpret_cast<bf16x2*>(&wsb[0][o]) = p1;
-        *reinterpret_cast<bf16x2*>(&wsb[1][o]) = p2;
-        *reinterpret_cast<bf16x2*>(&wsb[2][o]) = p3;
+    const int tiles = (n + 15) / 16;
+    const int tstride = gridDim.x * 4;
+    int tile = blockIdx.x * 4 + w;
+    // x fragments of one tile: KS k-steps x NL loads (rows past n clamp to n-1,
+    // k past fin to fin-LW: in bounds, and they meet zero W)
+    vec xr[KS][NL];
+    auto load_tile = [&](int tl) {
+        const int r = min(tl * 16 + cl, n - 1);
+        const float* xrow = X + (size_t)r * fin;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int q = 0; q < NL; ++q) {
+                const int k = min(32 * s + 8 * kq + LW * q, fin - LW);
+                xr[s][q] = *reinterpret_cast<const vec*>(xrow + k);
+            }
+    };
+    // the first tile's x loads go out before W's, so that the HBM latency of
+    // the one overlaps the W split (both are waited for at the split below)
+    load_tile(min(tile, tiles - 1));
+    // W split into three bf16 planes, zero past HF columns and past fin.  All
+    // of a thread's W loads are unconditional LW-wide loads at clamped
+    // addresses, issued together: a guarded scalar load per element made the
+    // split a chain of L2 round trips, one per loop iteration.
+    {
+        constexpr int WQ = (BN * KP + 256 * LW - 1) / (256 * LW);
+        vec wv[WQ];
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) {
+            const int e = (tid + 256 * q) * LW;  // KP % 32 == 0: e..e+LW-1 share a row
+            const int c = min(e / KP, HF - 1), k = min(e % KP, fin - LW);
+            wv[q] = *reinterpret_cast<const vec*>(W + (size_t)c * fin + k);
+        }
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) {
+            const int e = (tid + 256 * q) * LW;
+            if (e < BN * KP) {
+                const int c = e / KP, k = e % KP;
+                const bool ok = c < HF && k < fin;  // fin % LW == 0: the whole vector
+                const int o = c * WSB + k;
+                if constexpr (LW == 1) {
+                    bf16x2 p1, p2, p3;
+                    split3_pair(f32x2{ok ? wv[q] : 0.f, 0.f}, p1, p2, p3);
+                    wsb[0][o] = p1[0];
+                    wsb[1][o] = p2[0];
+                    wsb[2][o] = p3[0];
+                } else if constexpr (LW == 2) {
+                    bf16x2 p1, p2, p3;
+                    split3_pair(ok ? wv[q] : f32x2{0.f, 0.f}, p1, p2, p3);
+                    *reinterpret_cast<bf16x2*>(&wsb[0][o]) = p1;
+                    *reinterpret_cast<bf16x2*>(&wsb[1][o]) = p2;
+                    *reinterpret_cast<bf16x2*>(&wsb[2][o]) = p3;
+                } else {
+                    const f32x4 v = ok ? wv[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+                    bf16x2 p1a, p2a, p3a, p1b, p2b, p3b;
+                    split3_pair(f32x2{v.x, v.y}, p1a, p2a, p3a);
+                    split3_pair(f32x2{v.z, v.w}, p1b, p2b, p3b);
+                    *reinterpret_cast<bf16x4*>(&wsb[0][o]) = bf16x4{p1a[0], p1a[1], p1b[0], p1b[1]};
+                    *reinterpret_cast<bf16x4*>(&wsb[1][o]) = bf16x4{p2a[0], p2a[1], p2b[0], p2b[1]};
+                    *reinterpret_cast<bf16x4*>(&wsb[2][o]) = bf16x4{p3a[0], p3a[1], p3b[0], p3b[1]};
+                }
+            }
+        }
     }
     __syncthreads();
 
@@ -872,24 +923,6 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
         cs2[t] = c2[h];
     }
     float* Os = osm[w];
-    const int tiles = (n + 15) / 16;
-    const int tstride = gridDim.x * 4;
-    int tile = blockIdx.x * 4 + w;
-    // x fragments of one tile: KS k-steps x NL loads (rows past n clamp to n-1,
-    // k past fin to fin-LW: in bounds, and they meet zero W)
-    vec xr[KS][NL];
-    auto load_tile = [&](int tl) {
-        const int r = min(tl * 16 + cl, n - 1);
-        const float* xrow = X + (size_t)r * fin;
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-            for (int q = 0; q < NL; ++q) {
-                const int k = min(32 * s + 8 * kq + LW * q, fin - LW);
-                xr[s][q] = *reinterpret_cast<const vec*>(xrow + k);
-            }
-    };
-    load_tile(min(tile, tiles - 1));
     for (; tile < tiles; tile += tstride) {
         // split this tile's fragments (frees xr), then start the next tile's loads
         bf16x8 x1[KS], x2[KS], x3[KS];
@@ -2561,7 +2594,7 @@ const char* const kKnobNames[] = {
     "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_EDGE_LDS",  "GAT_EDGE_V",   "GAT_EDGE_U",
     "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
     "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
-    "GAT_PROJ_BM",     "GAT_PROJ_WRES"};
+    "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -2658,12 +2691,16 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     if (const char* v = knob("GAT_PROJ_WRES")) wres = std::atoi(v) != 0;
     if (pk != nullptr && std::strcmp(pk, "wres") != 0) wres = false;
     if (wres && fin > 0 && fin <= 128 && (nt == 1 || nt == 2 || nt == 4) && pow2_f && f <= 16) {
-        const uintptr_t xa = reinterpret_cast<uintptr_t>(x);
+        // x and W are both read LW floats at a time
+        const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
         const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
         const int ks = fin <= 32 ? 1 : fin <= 64 ? 2 : 4;
         const long long tiles = (n + 15) / 16;
-        // persistent beyond two workgroups per CU (each wave loops over tiles)
-        const int grid_w = (int)std::min<long long>((tiles + 3) / 4, 256 * 2);
+        // persistent beyond the workgroups one CU holds at once (each wave loops
+        // over tiles): 3 per CU for K <= 64 (45 KB of LDS, <= 168 VGPRs), else 2
+        int wg_cu = ks <= 2 ? 3 : 2;
+        if (const char* v = knob("GAT_PROJ_WRES_WGS")) wg_cu = std::max(1, std::atoi(v));
+        const int grid_w = (int)std::min<long long>((tiles + 3) / 4, 256LL * wg_cu);
 #define GAT_WRES(NTV, LWV, KSV)                                                               \
     hipLaunchKernelGGL((k_project_wres<NTV, LWV, KSV>), dim3(grid_w), dim3(256), 0, st, x, n, \
                        fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src,  \

@@ -56,7 +56,7 @@ def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_X3", "GAT_PROJ_WRES",
-              "GAT_PROJ_BM"):
+              "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
