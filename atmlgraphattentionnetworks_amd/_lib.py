@@ -18,7 +18,7 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 4
+GAT_ABI_VERSION = 5
 GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
 GAT_SEG_LOAD = 1
 GAT_SEG_STORE = 2
@@ -63,6 +63,10 @@ SIGNATURES = {
                                        _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
                                        _c_int, _c_int, _c_float, _c_float, _c_u64, _c_vp, _c_vp,
                                        _c_vp, _c_vp, _c_vp, _c_int, _c_vp]),
+    "gat_edge_aggregate_train": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
+                                          _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_float,
+                                          _c_float, _c_u64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                          _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_dropout_seed_next": (_c_int, [_c_vp, _c_vp, _c_vp]),
     "gat_csc_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csc_build": (_c_int, [_c_vp, _c_vp, _c_int, _c_ll, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
@@ -72,6 +76,8 @@ SIGNATURES = {
                                  _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
                                  _c_float, _c_float, _c_u64, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
                                  _c_vp]),
+    "gat_bwd_table": (_c_int, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
+                               _c_int, _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_bwd_sources_parts": (_c_int, [_c_int, _c_int, _c_int, _c_int_p]),
     "gat_bwd_sources": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_int,
                                  _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_float,

@@ -1403,7 +1403,14 @@ EdgeRows rows_of_csr(const int* rowptr) {
     return e;
 }
 
-template <int G, int U, int V, bool FUSED, bool PIPE = false>
+// KINK (training forward, recompute backward): also the per-head "kink sums"
+//   Q[i,h] = sum_j A_ij L'(z_ij) Wh[j,h]   and   R[i,h] = sum_j alpha_ij L'(z_ij)
+// (A = dropped coefficient, alpha = undropped, L' = 1 for z > 0 else slope).  The
+// backward's dL/ds_dst[i,h] = sum_j alpha_ij L'_ij (drop_ij dy_i.Wh_j - delta_i)
+// is then dy_i.Q_i - delta_i R_i: an elementwise kernel (k_bwd_table) instead of
+// a second pass over every in-edge (k_bwd_targets).  Q and R cost one more
+// accumulator per float4 and no gathers: the loop already holds Wh_j and p_ij.
+template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -1412,7 +1419,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const float* __restrict__ s_dst, int H, int F, int HF, int concat, float slope,
     const float* __restrict__ bias, float* __restrict__ out, int ld_out,
     float* __restrict__ lse, DropArgs drop_arg, float* __restrict__ y_heads,
-    int nslices, int slice_w, long long slice_stride) {
+    int nslices, int slice_w, long long slice_stride, float* __restrict__ q_heads,
+    float* __restrict__ r_heads) {
     const DropArgs drop = resolve_drop(drop_arg);
     // col values held per lane per chunk.  Groups of >= 4 lanes: every quad of
     // the group holds the chunk's indices (lane c: edges (c & 3) + 4t), so the
@@ -1462,10 +1470,10 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     // rows of >= 1024 edges keep Kahan-compensated running sums (lc, cmp) over
     // per-chunk partial sums: a 10k-edge hub row otherwise accumulates more fp32
     // error than the reference's own.  Shorter rows add directly (cheaper).
-    f32x4 acc[V], cmp[V];
-    float lc = 0.f;
+    f32x4 acc[V], cmp[V], accq[V];
+    float lc = 0.f, racc = 0.f;
 #pragma unroll
-    for (int q = 0; q < V; ++q) acc[q] = cmp[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < V; ++q) acc[q] = cmp[q] = accq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (er.load) {  // continue a row whose earlier segments a previous pass ran
         m = er.st_ml[(size_t)si * 2 * H + h];
         l = er.st_ml[(size_t)si * 2 * H + H + h];
@@ -1549,6 +1557,21 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         l *= scale;
 #pragma unroll
         for (int q = 0; q < V; ++q) acc[q] *= scale;
+        if constexpr (KINK) {
+            racc *= scale;
+#pragma unroll
+            for (int q = 0; q < V; ++q) accq[q] *= scale;
+        }
+        // kink sums of one edge (s[u] = LReLU(z) log2e has the sign of z)
+        auto kink = [&](int u, float p, float pa) {
+            if constexpr (KINK) {
+                const float lk = s[u] > 0.f ? 1.f : slope;
+                racc += p * lk;
+                const float pq = pa * lk;
+#pragma unroll
+                for (int q = 0; q < V; ++q) accq[q] += pq * v[u][q];
+            }
+        };
         if (!kahan) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -1558,6 +1581,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 if (dropping) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
                 for (int q = 0; q < V; ++q) acc[q] += pa * v[u][q];
+                kink(u, p, pa);
             }
         } else {
             lc *= scale;
@@ -1575,6 +1599,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 if (dropping) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
                 for (int q = 0; q < V; ++q) cs[q] += pa * v[u][q];
+                kink(u, p, pa);
             }
             // Kahan: add the chunk sums into the running sums
             const float y = ls - lc;
@@ -1651,6 +1676,14 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
         for (int q = 0; q < V; ++q)
             *reinterpret_cast<f32x4*>(y_heads + (size_t)r * HF + coff + 4 * q) = acc[q] * inv;
+    }
+    if constexpr (KINK) {
+        if (c_ok) {
+#pragma unroll
+            for (int q = 0; q < V; ++q)
+                *reinterpret_cast<f32x4*>(q_heads + (size_t)r * HF + coff + 4 * q) = accq[q] * inv;
+            if ((coff % F) == 0) r_heads[(size_t)r * H + h] = racc * inv;
+        }
     }
     if (concat) {
         if (c_ok) {
@@ -2157,6 +2190,55 @@ __global__ __launch_bounds__(256) void k_bwd_targets(
 }
 
 // ---------------------------------------------------------------------------
+// Pass 1 without edges (after the kink-sum forward, k_edge_grp<..., KINK>):
+// per target row i and head h, with dy = dL/dy_h and delta = dy . y,
+//   ds_dst[i,h] = dy . Q[i,h] - delta R[i,h]
+// (= sum_j alpha_ij L'(z_ij) (drop_ij dy . Wh_j - delta), the sum k_bwd_targets
+// walks the in-edges for), and the target table row exactly as k_bwd_targets
+// writes it.  G lanes per row (G = next_pow2(HF/4)), one float4 of one head each.
+// Per row: 4 ldg (g) + 8 HF (y, Q) + 12 H bytes read, 4 ld_t + 4 H written.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bwd_table(
+    int n, int G, const float* __restrict__ s_dst, const float* __restrict__ lse,
+    const float* __restrict__ y_heads, const float* __restrict__ q_heads,
+    const float* __restrict__ r_heads, const float* __restrict__ g, int H, int F, int HF,
+    int concat, float* __restrict__ ds_dst, float* __restrict__ T, int ld_t) {
+    const int lane = threadIdx.x & 63;
+    const int c = lane & (G - 1);
+    const long long r = (blockIdx.x * (long long)blockDim.x + threadIdx.x) / G;
+    if (r >= n) return;  // whole groups (G divides 64)
+    const bool c_ok = 4 * c < HF;
+    const int coff = c_ok ? 4 * c : 0;
+    const int h = coff / F;
+    const int hl = F / 4;
+    const bool leader = c_ok && (coff % F) == 0;
+    const int ldg = concat ? HF : F;
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 g4 = zero4, yv = zero4, qv = zero4;
+    const bool g_ok = c_ok && (concat || coff < F);
+    if (c_ok) {
+        g4 = *reinterpret_cast<const f32x4*>(g + r * ldg + (concat ? coff : coff % F));
+        yv = *reinterpret_cast<const f32x4*>(y_heads + r * HF + coff);
+        qv = *reinterpret_cast<const f32x4*>(q_heads + r * HF + coff);
+    }
+    const f32x4 dy = concat ? g4 : g4 * (1.f / (float)H);
+    auto hsum = [&](float v) {
+        if (hl <= 16) return group_sum16(v, hl);
+        for (int off = 1; off < hl; off <<= 1) v += __shfl_xor(v, off);
+        return v;
+    };
+    const float dl = hsum(dy.x * yv.x + dy.y * yv.y + dy.z * yv.z + dy.w * yv.w);
+    const float dq = hsum(dy.x * qv.x + dy.y * qv.y + dy.z * qv.z + dy.w * qv.w);
+    float* tr = T + r * ld_t;
+    if (g_ok) *reinterpret_cast<f32x4*>(tr + coff) = g4;
+    if (leader) {
+        ds_dst[r * H + h] = dq - dl * r_heads[r * H + h];
+        *reinterpret_cast<f32x4*>(tr + round_up4(ldg) + 4 * h) =
+            f32x4{s_dst[r * H + h], lse[r * H + h], dl, 0.f};
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Pass 2, per SOURCE row j (lane-group layout over the CSC): lane owns one
 // float4 of Wh[j] (one head).  Per out-edge j -> i (slot e, CSR position
 // k = csc_eid[e]): gather T[i] (the lane's g float4 + its head's
@@ -2594,7 +2676,7 @@ const char* const kKnobNames[] = {
     "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_EDGE_LDS",  "GAT_EDGE_V",   "GAT_EDGE_U",
     "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
     "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
-    "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS"};
+    "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS", "GAT_BWD_KINK"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -2838,7 +2920,7 @@ int gat_project_sliced(const float* x, int n, int fin, const float* w, const flo
 // Fused lane-group edge kernel, optionally with the gathers pipelined one
 // chunk ahead (GAT_EDGE_PIPE A/B knob): instantiated for the (U, V) pairs the
 // default schedule uses.
-template <int G, int U, int V, class... A>
+template <int G, int U, int V, bool KINK = false, class... A>
 static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A... a) {
     // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
     // kernel — caps the blocks resident per CU (160 KB / bytes)
@@ -2846,11 +2928,21 @@ static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A
     if (const char* el = knob("GAT_EDGE_LDS")) lds = (size_t)std::atol(el);
     if constexpr ((V == 1 && (U == 4 || U == 8)) || (V == 2 && (U == 8 || U == 16))) {
         if (pipe) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true>), grid, block, lds, st, a...);
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true, KINK>), grid, block, lds, st, a...);
             return;
         }
     }
-    hipLaunchKernelGGL((k_edge_grp<G, U, V, true>), grid, block, lds, st, a...);
+    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, KINK>), grid, block, lds, st, a...);
+}
+
+// the kink-sum forward is instantiated for the lane groups of HF = 64 heads
+// (G = 16 at V = 1, G = 8 at V = 2); kink_grp_ok says which launch it serves
+static bool kink_grp_ok(int g, int v) { return (g == 16 && v == 1) || (g == 8 && v == 2); }
+
+template <int G, int U, int V, class... A>
+static void launch_edge_kink(int pipe, dim3 grid, dim3 block, hipStream_t st, A... a) {
+    if constexpr ((G == 16 && V == 1) || (G == 8 && V == 2))
+        launch_edge_fused<G, U, V, true>(pipe, grid, block, st, a...);
 }
 
 extern "C" {
@@ -2862,7 +2954,8 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
                                int concat, int act, float negative_slope, const float* bias,
                                float* out, float* lse, float* y_heads, DropArgs drop,
                                int edges_per_row_hint, void* stream, int nslices = 1,
-                               long long slice_stride = 0) {
+                               long long slice_stride = 0, float* q_heads = nullptr,
+                               float* r_heads = nullptr) {
     if (act < GAT_ACT_LEAKY_RELU || act > GAT_ACT_HEAD_SOFTMAX) return GAT_EINVAL;
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin || nslices <= 0)
         return GAT_EINVAL;
@@ -2917,6 +3010,10 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     bool fused = grp_ok && pow2_hl && have_a;
     if (fused && s_src != nullptr) fused = kernel_choice("GAT_EDGE_SCORE", "gather");
     if (s_src == nullptr && !fused) return GAT_EUNSUPPORTED;
+    const bool kink = q_heads != nullptr;
+    if (kink && (!fused || sliced || r_heads == nullptr || lse == nullptr || y_heads == nullptr ||
+                 er.by_pos || er.load || er.store_lt > 0))
+        return GAT_EUNSUPPORTED;
     // a slice holds whole heads (the fused score sums a head inside one group)
     if (sliced && (!fused || slice_w % f != 0)) return GAT_EUNSUPPORTED;
     if (grp_ok && (s_src == nullptr || kernel_choice("GAT_EDGE_KERNEL", "generic"))) {
@@ -2936,12 +3033,15 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // rows keep more, shallower waves (PPI 30.5 -> 32.9 us pipelined)
         int pipe = (u == 16 && vv == 2) ? 1 : 0;
         if (const char* ep = knob("GAT_EDGE_PIPE")) pipe = std::atoi(ep);
+        if (kink && !kink_grp_ok(g, vv)) return GAT_EUNSUPPORTED;
 #define GAT_GRP_KARGS                                                                         \
     er, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,   \
         heads, f, hf, concat, negative_slope, bias, out, ld_out, lse, drop, y_heads, nslices,  \
-        slice_w, slice_stride
+        slice_w, slice_stride, q_heads, r_heads
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
-    if (fused)                                                                        \
+    if (kink)                                                                         \
+        launch_edge_kink<G, UU, VV>(pipe, grid, block, st, GAT_GRP_KARGS);             \
+    else if (fused)                                                                   \
         launch_edge_fused<G, UU, VV>(pipe, grid, block, st, GAT_GRP_KARGS);            \
     else                                                                              \
         hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, GAT_GRP_KARGS)
@@ -2970,6 +3070,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         return status_of(hipGetLastError());
     }
     // the generic kernel runs whole CSR rows only
+    if (kink) return GAT_EUNSUPPORTED;
     if (er.by_pos || er.load || er.store_lt > 0 || er.ee != er.eb + 1) return GAT_EUNSUPPORTED;
     const int* rowptr = er.eb;
     const int lpe = next_pow2((round_up4(hf) + 3) / 4);
@@ -3045,6 +3146,29 @@ int gat_edge_aggregate_ex(const int* rowptr, const int* col, const int* row_orde
                                ld_s, a_src, c_src, s_dst, heads, f, concat, score_act, act_param,
                                bias, out, lse, y_heads, make_drop(dropout_p, seed, seed_dev),
                                edges_per_row_hint, stream);
+}
+
+int gat_edge_aggregate_train(const int* rowptr, const int* col, const int* row_order,
+                             int row_begin, int row_end, const float* wh, int ld_wh,
+                             const float* a_src, const float* c_src, const float* s_dst,
+                             int heads, int f, int concat, float negative_slope, float dropout_p,
+                             unsigned long long seed, const unsigned long long* seed_dev,
+                             const float* bias, float* out, float* lse, float* y_heads,
+                             float* q_heads, float* r_heads, int edges_per_row_hint,
+                             void* stream) {
+    if (!(dropout_p >= 0.f && dropout_p <= 1.f)) return GAT_EINVAL;
+    if (row_end > row_begin && (a_src == nullptr || c_src == nullptr || lse == nullptr ||
+                                y_heads == nullptr || q_heads == nullptr || r_heads == nullptr))
+        return GAT_EINVAL;
+    // GAT_BWD_KINK=0 (A/B knob): refuse, so that the caller takes the
+    // gat_edge_aggregate_ex + gat_bwd_targets path
+    if (const char* v = knob("GAT_BWD_KINK"))
+        if (std::atoi(v) == 0) return GAT_EUNSUPPORTED;
+    return edge_aggregate_impl(rows_of_csr(rowptr), col, row_order, row_begin, row_end, wh, ld_wh,
+                               nullptr, 0, a_src, c_src, s_dst, heads, f, concat,
+                               GAT_ACT_LEAKY_RELU, negative_slope, bias, out, lse, y_heads,
+                               make_drop(dropout_p, seed, seed_dev), edges_per_row_hint, stream,
+                               1, 0, q_heads, r_heads);
 }
 
 int gat_edge_aggregate_seg(const int* seg_begin, const int* seg_end, int seg_by_pos,
@@ -3300,6 +3424,34 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
     }
 #undef GAT_BT_U
 #undef GAT_BT
+    return status_of(hipGetLastError());
+}
+
+int gat_bwd_table(const float* s_dst, const float* lse, const float* y_heads,
+                  const float* q_heads, const float* r_heads, const float* grad_out,
+                  int num_nodes, int heads, int f, int concat, float* ds_dst, float* table,
+                  int ld_t, void* stream) {
+    if (num_nodes < 0 || heads <= 0 || f <= 0) return GAT_EINVAL;
+    if (num_nodes > 0 && (s_dst == nullptr || lse == nullptr || y_heads == nullptr || q_heads == nullptr ||
+        r_heads == nullptr || grad_out == nullptr || ds_dst == nullptr || table == nullptr))
+        return GAT_EINVAL;
+    int need_ld = 0;
+    gat_bwd_table_layout(heads, f, concat, &need_ld);
+    if (ld_t < need_ld || (ld_t & 3)) return GAT_EINVAL;
+    const int hf = heads * f;
+    const int hl = f / 4;
+    if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS || f % 4 != 0 || next_pow2(hl) != hl)
+        return GAT_EUNSUPPORTED;
+    // GAT_BWD_KERNEL=stored|generic forces the stored-coefficient backward, as
+    // gat_bwd_targets honours it
+    if (const char* v = knob("GAT_BWD_KERNEL"))
+        if (std::strcmp(v, "stored") == 0 || std::strcmp(v, "generic") == 0) return GAT_EUNSUPPORTED;
+    if (num_nodes == 0) return GAT_OK;
+    const int g = next_pow2(hf / 4);
+    const long long threads = (long long)num_nodes * g;
+    hipLaunchKernelGGL(k_bwd_table, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, num_nodes, g, s_dst, lse, y_heads, q_heads, r_heads,
+                       grad_out, heads, f, hf, concat, ds_dst, table, ld_t);
     return status_of(hipGetLastError());
 }
 

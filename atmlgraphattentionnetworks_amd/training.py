@@ -6,11 +6,14 @@ PyG's gather/scatter ops (``run_inductive.py:83-90``, ``run_*_experiment.py``:
 ``loss.backward(); optimizer.step()``).  Here the gradient of
 ``GAT.py:37-67`` is computed by three library calls and two plain GEMMs:
 
-  forward   gat_project, then gat_edge_aggregate_ex (dropout GAT.py:61 from a
-            counter-based hash; any score activation; also stores lse and the
-            per-head aggregation y)
-  backward  1. gat_bwd_targets (per target row: dropout, softmax and LeakyReLU
-               backward -> ds_dst, and a per-target table [g | s_dst, lse, delta])
+  forward   gat_project, then gat_edge_aggregate_train (LeakyReLU, HF = 64:
+            also the per-head kink sums Q, R) or gat_edge_aggregate_ex (dropout
+            GAT.py:61 from a counter-based hash; any score activation; also
+            stores lse and the per-head aggregation y)
+  backward  1. gat_bwd_table after gat_edge_aggregate_train (elementwise:
+               ds_dst = dy.Q - delta R), else gat_bwd_targets (per target row
+               over the in-edges: dropout, softmax and LeakyReLU backward ->
+               ds_dst); both write the per-target table [g | s_dst, lse, delta]
             2. gat_bwd_sources (per source row over the CSC: recomputes each
                edge's coefficient from the table, dWh = sum A * dy + the score
                terms; per-wave partials of da/dc/db/dbias -- deterministic, no
@@ -83,14 +86,16 @@ class GATFunction(torch.autograd.Function):
         hfp = (hf + 3) // 4 * 4
         dev = x.device
         stream = torch._C._cuda_getCurrentRawStream(dev.index)
-        # one workspace: Wh | s_src | s_dst | lse | y
-        ws = torch.empty(n * (hfp + 3 * heads + hf), dtype=torch.float32, device=dev)
+        # one workspace: Wh | s_src | s_dst | lse | y | Q | R (Q, R: kink sums)
+        kink = act == _lib.GAT_ACT_LEAKY_RELU
+        ws = torch.empty(n * (hfp + 3 * heads + hf + (hf + heads if kink else 0)),
+                         dtype=torch.float32, device=dev)
         wh = ws[:n * hfp].view(n, hfp)
         o = n * hfp
         s_src = ws[o:o + n * heads].view(n, heads)
         s_dst = ws[o + n * heads:o + 2 * n * heads].view(n, heads)
         lse = ws[o + 2 * n * heads:o + 3 * n * heads].view(n, heads)
-        y = ws[o + 3 * n * heads:].view(n, hf)
+        y = ws[o + 3 * n * heads:o + 3 * n * heads + n * hf].view(n, hf)
         rc = lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                              pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
                              pp.c_dst.data_ptr(), heads, f, wh.data_ptr(), hfp,
@@ -99,16 +104,30 @@ class GATFunction(torch.autograd.Function):
             _lib.check(rc, "gat_project")
         out = torch.empty(n, hf if concat else f, dtype=torch.float32, device=dev)
         order = csr.order
-        rc = lib.gat_edge_aggregate_ex(
-            csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
-            0, n, wh.data_ptr(), hfp, s_src.data_ptr(), heads, pp.a_src.data_ptr(),
-            pp.c_src.data_ptr(), s_dst.data_ptr(), heads, f, int(concat), act, act_param, p,
-            seed, p_seed, bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(),
-            csr.kernel_hint(), stream)
-        if rc:
-            _lib.check(rc, "gat_edge_aggregate_ex")
+        if kink:
+            p_q = y.data_ptr() + 4 * n * hf
+            rc = lib.gat_edge_aggregate_train(
+                csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
+                0, n, wh.data_ptr(), hfp, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+                s_dst.data_ptr(), heads, f, int(concat), act_param, p, seed, p_seed,
+                bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(), p_q,
+                p_q + 4 * n * hf, csr.kernel_hint(), stream)
+            if rc and rc != _lib.GAT_EUNSUPPORTED:
+                _lib.check(rc, "gat_edge_aggregate_train")
+            kink = rc == 0  # GAT_EUNSUPPORTED: another head shape, or GAT_BWD_KINK=0
+        if not kink:
+            rc = lib.gat_edge_aggregate_ex(
+                csr.rowptr.data_ptr(), csr.col.data_ptr(),
+                0 if order is None else order.data_ptr(), 0, n, wh.data_ptr(), hfp,
+                s_src.data_ptr(), heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+                s_dst.data_ptr(), heads, f, int(concat), act, act_param, p, seed, p_seed,
+                bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(),
+                csr.kernel_hint(), stream)
+            if rc:
+                _lib.check(rc, "gat_edge_aggregate_ex")
         ctx.save_for_backward(x, ws)
         ctx.csr, ctx.pp, ctx.cfg, ctx.seed_slot = csr, pp, cfg, seed_slot
+        ctx.kink = kink
         return out
 
     @staticmethod
@@ -197,15 +216,23 @@ def _backward_recompute(ctx, g, ws, csc, stream):
     base = bw.data_ptr()
     order = csr.order
     hint = csr.kernel_hint()
-    rc = lib.gat_bwd_targets(
-        csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(), 0,
-        n, p_wh, hfp, pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, p_lse, p_y, g.data_ptr(),
-        heads, f, int(concat), act_param, p, seed, _seed_ptr(ctx), base, base + 4 * o_t, ld_t,
-        hint, stream)
+    if ctx.kink:
+        # the forward stored the kink sums Q | R after y: no pass over the in-edges
+        p_q = p_y + 4 * n * hf
+        rc = lib.gat_bwd_table(p_sd, p_lse, p_y, p_q, p_q + 4 * n * hf, g.data_ptr(), n, heads,
+                               f, int(concat), base, base + 4 * o_t, ld_t, stream)
+        name = "gat_bwd_table"
+    else:
+        rc = lib.gat_bwd_targets(
+            csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
+            0, n, p_wh, hfp, pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, p_lse, p_y,
+            g.data_ptr(), heads, f, int(concat), act_param, p, seed, _seed_ptr(ctx), base,
+            base + 4 * o_t, ld_t, hint, stream)
+        name = "gat_bwd_targets"
     if rc == _lib.GAT_EUNSUPPORTED:
         return None, None
     if rc:
-        _lib.check(rc, "gat_bwd_targets")
+        _lib.check(rc, name)
     rc = lib.gat_bwd_sources(
         csc.ptr.data_ptr(), csc.dst.data_ptr(), csc.eid.data_ptr(), n, p_wh, hfp,
         base + 4 * o_t, ld_t, base, pp.a_src.data_ptr(), pp.c_src.data_ptr(),

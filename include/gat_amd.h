@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 4
+#define GAT_ABI_VERSION 5
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -268,6 +268,27 @@ int gat_edge_aggregate_ex(const int* rowptr, const int* col, const int* row_orde
                           int edges_per_row_hint, void* stream);
 
 /*
+ * Training forward for the recompute backward (LeakyReLU with slope in [0, 1],
+ * heads*f = 64 lane groups; GAT_EUNSUPPORTED otherwise -- then use
+ * gat_edge_aggregate_ex + gat_bwd_targets).  As gat_edge_aggregate_ex with
+ * score_act = GAT_ACT_LEAKY_RELU (s_src recomputed from the gathered Wh row), and
+ * also the per-head kink sums the backward needs for dL/ds_dst:
+ *   q_heads  [rows, heads*f]: Q[i,h] = sum_j A_ij L'(z_ij) Wh[j,h]
+ *   r_heads  [rows, heads]:   R[i,h] = sum_j alpha_ij L'(z_ij)
+ * with A the dropped and alpha the undropped coefficient, L' = 1 for z > 0 and
+ * negative_slope otherwise.  lse and y_heads are required.  Replaces
+ * GAT.py:53-67 in training mode; gat_bwd_table then replaces gat_bwd_targets.
+ */
+int gat_edge_aggregate_train(const int* rowptr, const int* col, const int* row_order,
+                             int row_begin, int row_end, const float* wh, int ld_wh,
+                             const float* a_src, const float* c_src, const float* s_dst,
+                             int heads, int f, int concat, float negative_slope, float dropout_p,
+                             unsigned long long seed, const unsigned long long* seed_dev,
+                             const float* bias, float* out, float* lse, float* y_heads,
+                             float* q_heads, float* r_heads, int edges_per_row_hint,
+                             void* stream);
+
+/*
  * Device-side dropout seeds: *seed_out = splitmix64(*counter); *counter += 1, on
  * `stream`.  Pass seed_out as `seed_dev` to the forward and to the backward of the
  * same call.  Inside a captured HIP graph each replay advances the counter, so
@@ -318,6 +339,17 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
                     float negative_slope, float dropout_p, unsigned long long seed,
                     const unsigned long long* seed_dev, float* ds_dst, float* table, int ld_t,
                     int edges_per_row_hint, void* stream);
+
+/*
+ * Pass 1 without an edge loop, after gat_edge_aggregate_train: per TARGET row
+ *   ds_dst[i,h] = dy_h . q_heads[i,h] - delta_h r_heads[i,h],  delta_h = dy_h . y_h
+ * (the same sum gat_bwd_targets walks the in-edges for) and the same target
+ * table as gat_bwd_targets.  All nodes, rows in node order.
+ */
+int gat_bwd_table(const float* s_dst, const float* lse, const float* y_heads,
+                  const float* q_heads, const float* r_heads, const float* grad_out,
+                  int num_nodes, int heads, int f, int concat, float* ds_dst, float* table,
+                  int ld_t, void* stream);
 
 /* Number of partial rows gat_bwd_sources writes for this shape (a multiple of 4). */
 int gat_bwd_sources_parts(int num_nodes, int heads, int f, int* num_parts);

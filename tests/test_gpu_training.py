@@ -145,6 +145,57 @@ def test_dropout_forward_and_backward(case, p, kernel, monkeypatch):
     assert abs(kept - (1 - p)) < 0.05
 
 
+@pytest.mark.parametrize("p", [0.0, 0.6])
+@pytest.mark.parametrize("shape", ["ppi_u4", "reddit_pipe", "mean"])
+def test_kink_sums_backward_equals_edge_pass(shape, p, monkeypatch):
+    """The kink-sum forward (gat_edge_aggregate_train) + gat_bwd_table give the
+    gradients the edge-walking pass 1 (gat_edge_aggregate_ex + gat_bwd_targets,
+    GAT_BWD_KINK=0) gives, on the V = 1 (PPI) and pipelined V = 2 (Reddit)
+    kernels, and both match the float64 oracle."""
+    if shape == "reddit_pipe":
+        monkeypatch.setenv("GAT_EDGE_PIPE", "1")
+        monkeypatch.setenv("GAT_EDGE_U", "16")
+        monkeypatch.setenv("GAT_EDGE_V", "2")
+    concat = shape != "mean"
+    n, e, fin, H, F = 700, 9000, 50, 8, 8
+    layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat, seed=11)
+    seed = 0xC0FFEE
+    drop = torch.from_numpy(dropout_factors(csr_positions(ei, n), H, p, seed)) if p else None
+    gout = torch.randn(n, H * F if concat else F, generator=torch.Generator().manual_seed(8))
+    res = {}
+    for kink in ("1", "0"):
+        monkeypatch.setenv("GAT_BWD_KINK", kink)
+        xd, out = _run(layer, x, ei, p, seed)
+        assert out.grad_fn is not None
+        _check_grads(layer, state, xd, out, ei, x, H, concat, gout, drop)
+        res[kink] = [xd.grad.clone()] + [q.grad.clone() for q in layer.parameters()]
+    for a, b in zip(res["1"], res["0"]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()) + 1e-7)
+
+
+def test_kink_sums_used_for_hf64():
+    """The default training forward at HF = 64 takes the kink-sum kernel (no
+    edge pass in the backward); other head widths fall back to the edge pass."""
+    from atmlgraphattentionnetworks_amd.graph import get_csr
+    from atmlgraphattentionnetworks_amd.training import GATFunction, gat_train_forward
+    seen = []
+    orig = GATFunction.forward
+
+    def spy(ctx, *a):
+        out = orig(ctx, *a)
+        seen.append(ctx.kink)
+        return out
+    GATFunction.forward = staticmethod(spy)
+    try:
+        for (n, e, fin, H, F, concat) in (CASES[0], CASES[6]):
+            layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat)
+            csr = get_csr(ei.to(DEV), n)
+            gat_train_forward(layer, x.to(DEV).requires_grad_(True), csr, 0.0, 0)
+    finally:
+        GATFunction.forward = orig
+    assert seen == [True, False]
+
+
 def test_train_forward_without_dropout_equals_eval_forward():
     n, e, fin, H, F, concat = CASES[0]
     layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat)

@@ -110,6 +110,19 @@ def test_training_entry_points_validate_without_gpu():
     assert tgt(ld_t=90) == EINVAL
     assert tgt(f=7, ld_t=96) == EUNS  # f % 4 != 0 -> stored-coefficient path
     assert tgt(slope=-0.5) == EUNS
+    # kink-sum training forward and its edge-free pass 1: missing outputs or a
+    # bad dropout probability are EINVAL before any launch
+    def train(p=0.0, q=None):
+        return lib.gat_edge_aggregate_train(None, None, None, 0, 10, None, 64, 8, 8, None, 8, 8,
+                                            1, 0.2, p, 0, None, None, None, 8, 8, q, 8, 0, None)
+    assert train(q=None) == EINVAL  # q_heads required (for a non-empty row range)
+    assert train(p=1.5, q=8) == EINVAL
+    def table(f=8, ld_t=96, n=10, ptr=8):
+        return lib.gat_bwd_table(ptr, 8, 8, 8, 8, 8, n, 8, f, 1, 8, 8, ld_t, None)
+    assert table(ptr=None) == EINVAL
+    assert table(ld_t=92) == EINVAL
+    assert table(f=6, ld_t=96) == EUNS  # f % 4 != 0
+    assert table(n=0) == OK  # nothing to do
     parts = ctypes.c_int()
     assert lib.gat_bwd_sources_parts(1000, 8, 8, ctypes.byref(parts)) == OK
     assert parts.value % 4 == 0 and parts.value >= 4
