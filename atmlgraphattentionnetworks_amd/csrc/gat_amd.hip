@@ -2522,7 +2522,13 @@ __global__ __launch_bounds__(64) void k_src_bwd(
 // part[s] = the chunk's [HF, Fin] partial; k_wgrad_reduce sums the chunks in
 // a fixed order (deterministic).
 // Algorithmic bytes: 4 N (HF + Fin) reads + 4 S HF Fin partials.
+// LW > 1: the four 16-column sub-tiles are interleaved so that a lane's four x
+// values of a row are LW adjacent floats (sub-tile t, lane column ii holds
+// fin column j0 + LW ii + (t % LW) + 16 LW (t / LW)): one float2 / float4 load
+// instead of four scalar ones (the B columns of an MFMA may be any 16 columns;
+// the store maps them back).  The kernel is bound by load instructions.
 // ---------------------------------------------------------------------------
+template <int LW>
 __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dwh, int ld_dwh,
                                                const float* __restrict__ x, int n, int fin,
                                                int hf, int rows_per_chunk,
@@ -2539,9 +2545,14 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dwh, in
     const bool i_ok = icol < hf;
     const float amask = i_ok ? 1.f : 0.f;
     const int ic = i_ok ? icol : 0;
-    int jc[4];
+    // column of sub-tile t held by this lane
+    auto jcol = [&](int t) {
+        return LW == 1 ? j0 + 16 * t + ii : j0 + LW * ii + (t % LW) + 16 * LW * (t / LW);
+    };
+    constexpr int NLD = 4 / LW;  // x loads per row
+    int jc[NLD];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) jc[t] = min(j0 + 16 * t + ii, fin - 1);
+    for (int q = 0; q < NLD; ++q) jc[q] = min(jcol(q * LW), fin - LW);  // in bounds; unused past fin
     f32x4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2554,8 +2565,19 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dwh, in
             const bool ok = row < r1;
             const int rr = ok ? row : r1 - 1;
             av[u] = dwh[(size_t)rr * ld_dwh + ic] * (ok ? amask : 0.f);
+            const float* xr = x + (size_t)rr * fin;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) bv[u][t] = x[(size_t)rr * fin + jc[t]];
+            for (int q = 0; q < NLD; ++q) {
+                if constexpr (LW == 4) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(xr + jc[q]);
+                    bv[u][0] = v.x; bv[u][1] = v.y; bv[u][2] = v.z; bv[u][3] = v.w;
+                } else if constexpr (LW == 2) {
+                    const f32x2 v = *reinterpret_cast<const f32x2*>(xr + jc[q]);
+                    bv[u][2 * q] = v.x; bv[u][2 * q + 1] = v.y;
+                } else {
+                    bv[u][q] = xr[jc[q]];
+                }
+            }
         }
 #pragma unroll
         for (int u = 0; u < UR; ++u)
@@ -2567,7 +2589,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dwh, in
     float* ps = part + (size_t)s * hf * fin;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const int j = j0 + 16 * t + ii;
+        const int j = jcol(t);
         if (j >= fin) continue;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -2676,7 +2698,8 @@ const char* const kKnobNames[] = {
     "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_EDGE_LDS",  "GAT_EDGE_V",   "GAT_EDGE_U",
     "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
     "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
-    "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS", "GAT_BWD_KINK"};
+    "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS", "GAT_BWD_KINK",
+    "GAT_WGRAD_LW"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -3631,8 +3654,20 @@ int gat_weight_grad(const float* x, int num_nodes, int fin, const float* dwh, in
     const int rows = (num_nodes + chunks - 1) / chunks;
     float* part = (float*)workspace;
     const dim3 grid((fin + 63) / 64, chunks, (hf + 63) / 64), block(256);
-    hipLaunchKernelGGL(k_wgrad, grid, block, 0, st, dwh, ld_dwh, x, num_nodes, fin, hf, rows,
-                       part);
+    // x rows read LW floats at a time where fin and x's alignment allow
+    // (GAT_WGRAD_LW A/B knob caps it)
+    const uintptr_t xa = reinterpret_cast<uintptr_t>(x);
+    int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
+    if (const char* v = knob("GAT_WGRAD_LW")) lw = std::min(lw, std::max(1, std::atoi(v)));
+    if (lw == 4)
+        hipLaunchKernelGGL(k_wgrad<4>, grid, block, 0, st, dwh, ld_dwh, x, num_nodes, fin, hf,
+                           rows, part);
+    else if (lw == 2)
+        hipLaunchKernelGGL(k_wgrad<2>, grid, block, 0, st, dwh, ld_dwh, x, num_nodes, fin, hf,
+                           rows, part);
+    else
+        hipLaunchKernelGGL(k_wgrad<1>, grid, block, 0, st, dwh, ld_dwh, x, num_nodes, fin, hf,
+                           rows, part);
     const long long count = (long long)hf * fin;
     hipLaunchKernelGGL(k_colsum, dim3((unsigned)((count + 15) / 16)), dim3(256), 0, st, part,
                        chunks, count, dw, chunks);
