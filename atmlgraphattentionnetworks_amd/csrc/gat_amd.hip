@@ -106,9 +106,19 @@ struct DropArgs {
     unsigned thresh;   // 0: no dropout
     float scale;       // 1 / (1 - p)
     unsigned seed_lo, seed_hi;
-    unsigned b0;       // mix32(seed_hi): the high-word hash of every index below 2^32
     const unsigned long long* seed_ptr;  // if set, the seed is read from device memory
 };
+
+// The seed may live in device memory (gat_dropout_seed_next), so that a
+// captured HIP graph draws a fresh mask on every replay.
+__device__ __forceinline__ DropArgs resolve_drop(DropArgs d) {
+    if (d.seed_ptr != nullptr) {
+        const unsigned long long sv = *d.seed_ptr;
+        d.seed_lo = (unsigned)sv;
+        d.seed_hi = (unsigned)(sv >> 32);
+    }
+    return d;
+}
 
 __host__ __device__ __forceinline__ unsigned mix32(unsigned x) {
     x ^= x >> 16;
@@ -119,25 +129,11 @@ __host__ __device__ __forceinline__ unsigned mix32(unsigned x) {
     return x;
 }
 
-// The seed may live in device memory (gat_dropout_seed_next), so that a
-// captured HIP graph draws a fresh mask on every replay.
-__device__ __forceinline__ DropArgs resolve_drop(DropArgs d) {
-    if (d.seed_ptr != nullptr) {
-        const unsigned long long sv = *d.seed_ptr;
-        d.seed_lo = (unsigned)sv;
-        d.seed_hi = (unsigned)(sv >> 32);
-        d.b0 = mix32(d.seed_hi);
-    }
-    return d;
-}
-
 // multiplier applied to a coefficient: scale if kept, 0 if dropped
 __device__ __forceinline__ float drop_factor(const DropArgs& d, long long k, int h, int H) {
     const unsigned long long idx = (unsigned long long)k * (unsigned)H + (unsigned)h;
     const unsigned a = mix32((unsigned)idx ^ d.seed_lo);
-    // every position below 2^32 / H shares the high word 0: its hash is hoisted into b0
-    const unsigned hi = (unsigned)(idx >> 32);
-    const unsigned b = __builtin_expect(hi == 0u, 1) ? d.b0 : mix32(hi + d.seed_hi);
+    const unsigned b = mix32((unsigned)(idx >> 32) + d.seed_hi);
     return mix32(a ^ b) >= d.thresh ? d.scale : 0.f;
 }
 
@@ -153,7 +149,6 @@ DropArgs make_drop(float p, unsigned long long seed,
     d.scale = p <= 0.f ? 1.f : p >= 1.f ? 0.f : 1.f / (1.f - p);
     d.seed_lo = (unsigned)seed;
     d.seed_hi = (unsigned)(seed >> 32);
-    d.b0 = mix32(d.seed_hi);
     return d;
 }
 
