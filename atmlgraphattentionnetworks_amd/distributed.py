@@ -139,12 +139,19 @@ def fused_score_ok(heads: int, f: int, act: int, param: float) -> bool:
             and (hl & (hl - 1)) == 0)
 
 
-def default_chunks(world: int, local_edges: int, fused: bool) -> int:
-    """All-gather chunks (= edge passes) per step: one pass per ~4M local edges,
-    at most 4; 1 on a single rank or without the fused kernels."""
+EDGES_PER_CHUNK = 4_000_000  # per-rank edges per all-gather chunk / edge pass
+
+
+def default_chunks(world: int, total_edges: int, fused: bool) -> int:
+    """All-gather chunks (= edge passes) per step: one pass per ~4M edges per
+    rank, at most 4; 1 on a single rank or without the fused kernels.
+
+    Every rank must pick the SAME count (it fixes the table layout and the
+    collectives' sizes), so the argument is the graph's total edge count E',
+    which all ranks see, never a rank's own share."""
     if world <= 1 or not fused:
         return 1
-    return max(1, min(4, local_edges // 4_000_000))
+    return max(1, min(4, (total_edges // world) // EDGES_PER_CHUNK))
 
 
 class HipOps:
@@ -258,11 +265,15 @@ class ShardedGAT:
 
     def __init__(self, layer, csr, world: int, rank: int, exchange: str = "allgather",
                  group=None, ops=None, packed=None, chunks: Optional[int] = None,
-                 exchanger=None):
+                 exchanger=None, force_exchange: bool = False):
+        """force_exchange: issue the chunk collectives even at world 1 (an
+        in-place all-gather of a rank's own block), so the RCCL path can be
+        exercised on a one-GPU box (tests, ``bench.py --dist``)."""
         if exchange not in ("allgather", "replicate"):
             raise ValueError(exchange)
         self.layer, self.world, self.rank = layer, world, rank
         self.exchange = exchange
+        self.force_exchange = bool(force_exchange)
         self.ops = ops or HipOps
         self.heads, self.f = layer.num_heads, layer.output_channels
         self.concat = layer.concat
@@ -295,7 +306,7 @@ class ShardedGAT:
         else:
             width, s_off = _lib.table_layout(heads, f)
         if exchange == "allgather":
-            k = chunks if chunks is not None else default_chunks(world, e1 - e0, self.fused)
+            k = chunks if chunks is not None else default_chunks(world, csr.num_edges, self.fused)
             if not self.fused:
                 k = 1
             k = max(1, min(k, self.rows_per_part))
@@ -328,8 +339,8 @@ class ShardedGAT:
         else:
             self.st_acc = self.st_ml = None
         if exchanger is None:
-            exchanger = CollectiveExchange(group) if (exchange == "allgather" and world > 1) \
-                else NoExchange()
+            exchanger = CollectiveExchange(group) if (
+                exchange == "allgather" and (world > 1 or self.force_exchange)) else NoExchange()
         self.exchanger = exchanger
 
     def _local_csr(self, csr, e0: int, e1: int, dev) -> LocalCSR:
@@ -388,7 +399,7 @@ class ShardedGAT:
                               lay.block_offset(c, self.rank), self.s_dst[lo:hi], self.s_scratch)
 
     def exchange_start(self, c: int):
-        if self.exchange != "allgather" or self.world == 1:
+        if self.exchange != "allgather" or (self.world == 1 and not self.force_exchange):
             return None
         lo, hi = self.layout.chunk_range(c)
         off = self.layout.block_offset(c, self.rank)
@@ -439,13 +450,25 @@ def emulate(layer, csr, x, world: int, exchange: str = "allgather",
     all-gather emulated by block copies, every rank's edge passes; returns the
     concatenated output [N, width].  Runs the real kernels on the real
     per-rank tables, segments and state buffers."""
+    ranks, xs = _emulated_ranks(layer, csr, x, world, exchange, chunks)
+    outs = [sh.phase_edges() for sh in ranks]
+    return torch.cat(outs)
+
+
+def _emulated_ranks(layer, csr, x, world: int, exchange: str, chunks: Optional[int]):
+    """Every rank's ShardedGAT in one process, projected, tables filled by
+    block copies (the all-gather's result)."""
     ranks = [ShardedGAT(layer, csr, world, r, exchange=exchange, chunks=chunks,
                         exchanger=NoExchange()) for r in range(world)]
+    lay = ranks[0].layout
+    for sh in ranks[1:]:
+        # the layout fixes the collectives' sizes: every rank must agree
+        if sh.layout != lay:
+            raise RuntimeError(f"rank {sh.rank} table layout {sh.layout} != rank 0's {lay}")
     xs = [sh.local_x(x) for sh in ranks]
     for sh, xl in zip(ranks, xs):
         sh.phase_project(xl)
     if exchange == "allgather" and world > 1:
-        lay = ranks[0].layout
         for c in range(lay.chunks):
             for src in ranks:
                 off = lay.block_offset(c, src.rank)
@@ -453,8 +476,37 @@ def emulate(layer, csr, x, world: int, exchange: str = "allgather",
                 for dst in ranks:
                     if dst is not src:
                         dst.table[off:off + lay.block_floats].copy_(blk)
-    outs = [sh.phase_edges() for sh in ranks]
-    return torch.cat(outs)
+    return ranks, xs
+
+
+def emulate_rank_times(layer, csr, x, world: int, exchange: str = "allgather",
+                       chunks: Optional[int] = None, iters: int = 20) -> Dict:
+    """The COMPUTE side of one partitioned step, measured on one GPU: for each
+    of ``world`` emulated ranks, its projection (``phase_project``) and its
+    edge passes (``phase_edges``) alone, HIP events on the current stream, on
+    the rank's real table, local CSR and segments.  A rank of a real
+    multi-GPU run does exactly this work on its own GPU, plus the collective;
+    the max over ranks bounds the step from below (SURVEY.md §8e cost model)."""
+    ranks, xs = _emulated_ranks(layer, csr, x, world, exchange, chunks)
+    per = []
+    for sh, xl in zip(ranks, xs):
+        proj = _event_ms(lambda: sh.phase_project(xl), iters)
+        edge = _event_ms(sh.phase_edges, iters)
+        per.append({"rank": sh.rank, "rows": sh.n_local, "local_edges": sh.local.num_edges,
+                    "project_ms": proj, "edge_passes_ms": edge})
+    lay = ranks[0].layout
+    blk_bytes = 4 * lay.block_floats
+    recv = blk_bytes * lay.chunks * (world - 1) if exchange == "allgather" else 0
+    res = {"ranks": world, "exchange": exchange, "chunks": lay.chunks,
+           "table_layout": lay.kind, "table_bytes_per_rank": 4 * lay.numel,
+           "collective_bytes_received_per_rank": recv,
+           "max_project_ms": max(p["project_ms"] for p in per),
+           "max_edge_passes_ms": max(p["edge_passes_ms"] for p in per),
+           "max_compute_ms": max(p["project_ms"] + p["edge_passes_ms"] for p in per),
+           "per_rank": per}
+    del ranks, xs
+    torch.cuda.empty_cache()
+    return res
 
 
 def gather_output(local_out: torch.Tensor, bounds: List[int], group=None) -> torch.Tensor:
@@ -514,12 +566,29 @@ def _make_layer(w, dev):
                                concat=w.concat).to(dev).eval()
 
 
-def _sharded_workload(w, dev, world: int, rank: int, exchanger, args, chunk_choices) -> Dict:
+def _max_over_ranks(v: float) -> float:
+    t = torch.tensor([v], dtype=torch.float64)  # default group: gloo, on the host
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _strategy_key(exchange: str, chunks: int) -> str:
+    return "replicate" if exchange == "replicate" else f"allgather_k{chunks}"
+
+
+def _sharded_workload(w, dev, world: int, rank: int, exchanger, args, strategies,
+                      force_exchange: bool = False) -> Dict:
     """ONE shared graph of workload w, node-range partitioned over the ranks
-    (SURVEY.md §8e): per step, project own rows -> chunked RCCL all-gather ->
-    edge passes.  Also on rank 0: the same layer forward on the whole graph on
-    one GPU (the 1-GPU reference for this workload) and a check that the
-    gathered sharded output equals it."""
+    (SURVEY.md §8e).  Each strategy in ``strategies`` — (exchange, chunks):
+    ("allgather", K) = project own rows -> K-chunk all-gather of the node table
+    over the exchanger (RCCL) -> K edge passes overlapped with it;
+    ("replicate", 1) = every rank projects all rows, no collective — is timed
+    for a few steps; the fastest is timed for the full K steps and is the
+    workload's ``value``.  The best all-gather strategy is always reported
+    beside it (``allgather``) with its collective and compute phases alone.
+    Also on rank 0: the same layer forward on the whole graph on one GPU (the
+    1-GPU reference for this workload) and a check that every reported
+    strategy's gathered output equals it."""
     from .graph import build_csr
     from .synthetic import make_inputs
 
@@ -527,7 +596,7 @@ def _sharded_workload(w, dev, world: int, rank: int, exchanger, args, chunk_choi
     csr = build_csr(ei, x.size(0))
     layer = _make_layer(w, dev)
     res = {"workload": w.name, "N": x.size(0), "E_prime": csr.num_edges,
-           "Fin": w.in_channels, "H": w.heads, "F": w.out_channels}
+           "Fin": w.in_channels, "H": w.heads, "F": w.out_channels, "concat": w.concat}
     ref = None
     with torch.no_grad():
         if rank == 0:  # the single-GPU forward of the same workload (others wait)
@@ -538,7 +607,7 @@ def _sharded_workload(w, dev, world: int, rank: int, exchanger, args, chunk_choi
             def one():
                 return gat_forward(x, csr, pp, bias, w.heads, w.out_channels, w.concat,
                                    layer.negative_slope)
-            for _ in range(3):
+            for _ in range(max(3, args.warmup)):
                 ref = one()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -552,47 +621,74 @@ def _sharded_workload(w, dev, world: int, rank: int, exchanger, args, chunk_choi
                                       "GPU alone (bench.py's single-GPU path)"}
         dist.barrier()
         del ei
-        # chunk count: try each candidate for a few steps, keep the fastest
+        # try each strategy for a few steps (every rank runs the same list: the
+        # layout, hence the skip decision, depends only on global values)
         tried = {}
-        best = None
-        for k in chunk_choices:
-            sh = ShardedGAT(layer, csr, world, rank, chunks=k, exchanger=exchanger)
-            if sh.chunks != k and k != 1:
+        built = {}
+        for exch, k in strategies:
+            sh = ShardedGAT(layer, csr, world, rank, exchange=exch, chunks=k,
+                            exchanger=exchanger if exch == "allgather" else NoExchange(),
+                            force_exchange=force_exchange)
+            if exch == "allgather" and sh.chunks != k:
                 continue
+            key = _strategy_key(exch, k)
             xl = sh.local_x(x)
             t = _time_steps(lambda: sh.forward(xl), 2, 5)
-            tried[k] = t * 1e3 / 5
-            if best is None or tried[k] < tried[best[0]]:
-                best = (k, sh, xl)
-            else:
-                del sh
-        k, sh, xl = best
-        t = _time_steps(lambda: sh.forward(xl), args.warmup, args.steps)
-        ms = t * 1e3 / args.steps
-        # the pieces alone (max over ranks): collective, projection, edge passes
-        t_ex = _time_steps(sh.phase_exchange, 2, args.steps) * 1e3 / args.steps \
-            if world > 1 else 0.0
-        proj_ms = _event_ms(lambda: sh.phase_project(xl), args.steps)
-        edge_ms = _event_ms(sh.phase_edges, args.steps)
-        # check: gathered sharded output == the single-GPU forward
-        sh.forward(xl)
-        full = gather_output(sh.out, sh.bounds)
-    res.update({
-        "value": csr.num_edges / (ms * 1e-3), "unit": "edges/s", "ms_per_step": ms,
-        "chunks": k, "chunk_trials_ms": tried, "collective_ms": t_ex,
-        "rank0_project_ms": proj_ms, "rank0_edge_passes_ms": edge_ms,
-        "rows_per_rank": sh.rows_per_part, "table_bytes": int(sh.table.numel() * 4),
-        "table_layout": sh.layout.kind, "planes": sh.slices,
-        "rank0_local_edges": sh.local.num_edges,
-    })
+            tried[key] = t * 1e3 / 5
+            built[key] = (sh, xl)
+        best = min(tried, key=tried.get)
+        ag = [k_ for k_ in tried if k_.startswith("allgather")]
+        best_ag = min(ag, key=tried.get) if ag else None
+        for key in list(built):  # free the losers' tables
+            if key not in (best, best_ag):
+                del built[key]
+        torch.cuda.empty_cache()
+
+        def measure(key):
+            sh, xl = built[key]
+            t = _time_steps(lambda: sh.forward(xl), args.warmup, args.steps)
+            ms = t * 1e3 / args.steps
+            d = {"strategy": key, "exchange": sh.exchange, "chunks": sh.chunks,
+                 "value": csr.num_edges / (ms * 1e-3), "ms_per_step": ms}
+            # the pieces alone (max over ranks): collective, projection, edge passes
+            if sh.exchange == "allgather" and (world > 1 or force_exchange):
+                d["collective_ms"] = _time_steps(sh.phase_exchange, 2, args.steps) * 1e3 / \
+                    args.steps
+            d["project_ms_max_over_ranks"] = _max_over_ranks(
+                _event_ms(lambda: sh.phase_project(xl), args.steps))
+            d["edge_passes_ms_max_over_ranks"] = _max_over_ranks(
+                _event_ms(sh.phase_edges, args.steps))
+            lay = sh.layout
+            d.update({"rows_per_rank": sh.rows_per_part, "table_bytes": int(sh.table.numel() * 4),
+                      "table_layout": lay.kind, "planes": sh.slices,
+                      "rank0_local_edges": sh.local.num_edges if rank == 0 else None,
+                      "collective_bytes_received_per_rank":
+                          4 * lay.block_floats * lay.chunks * (world - 1)
+                          if sh.exchange == "allgather" else 0})
+            # check: gathered sharded output == the single-GPU forward
+            sh.forward(xl)
+            full = gather_output(sh.out, sh.bounds)
+            if rank == 0:
+                diff = float((full - ref).abs().max())
+                scale = float(ref.abs().max())
+                d["check"] = {"max_abs_diff_vs_one_gpu": diff, "max_abs_ref": scale}
+                if not diff <= 1e-5 + 1e-5 * scale:
+                    raise RuntimeError(f"sharded {w.name} ({key}) output differs from the "
+                                       f"single-GPU forward: max |diff| {diff:.3e} "
+                                       f"(max |ref| {scale:.3e})")
+            return d
+
+        head = measure(best)
+        agd = head if best_ag in (None, best) else measure(best_ag)
+    res.update({k_: v for k_, v in head.items()})
+    res["unit"] = "edges/s"
+    res["strategy_trials_ms"] = tried
+    res["allgather"] = agd if best_ag is not None else None
     if rank == 0:
-        diff = float((full - ref).abs().max())
-        scale = float(ref.abs().max())
-        res["check"] = {"max_abs_diff_vs_one_gpu": diff, "max_abs_ref": scale}
-        if not diff <= 1e-5 + 1e-5 * scale:
-            raise RuntimeError(f"sharded {w.name} output differs from the single-GPU forward: "
-                               f"max |diff| {diff:.3e} (max |ref| {scale:.3e})")
-    del sh, x, csr
+        res["speedup_vs_one_gpu"] = res["value"] / res["one_gpu"]["value"]
+        if best_ag is not None:
+            res["allgather"]["speedup_vs_one_gpu"] = agd["value"] / res["one_gpu"]["value"]
+    del built, x, csr
     torch.cuda.empty_cache()
     return res
 
@@ -618,13 +714,19 @@ def _ppi_blocks_weak(w, dev, world: int, rank: int, args) -> Dict:
 
 
 def bench_distributed(args, metric: str):
-    """One process per GPU (torchrun).  The reported line is the north-star
-    path on ONE shared Reddit-scale graph (BASELINE.json
-    configs[4]): node-range partition, chunked RCCL all-gather of the node
-    table inside the timed step, edge passes overlapped with it.  Strong
-    scaling: total work is fixed as N grows.  ogbn-arxiv scale (configs[3])
-    runs the same way under "workloads"; the data-parallel PPI-block run is a
-    secondary field."""
+    """One process per GPU (torchrun).  The reported line is BASELINE.json's
+    metric on its own workload: the PPI-shape graph (configs[1]) as ONE
+    shared graph, node-range partitioned over the ranks, the
+    exchange inside the timed step.  Strong scaling: total work is fixed as N
+    grows, so ``value`` at N GPUs compares directly with the N = 1 line's PPI
+    ``value``.  Reddit scale (configs[4]) and ogbn-arxiv scale (configs[3])
+    run the same way under ``workloads``, each with its own one-GPU time and
+    ``speedup_vs_one_gpu``; the data-parallel PPI-block run is a secondary
+    field.
+
+    At WORLD_SIZE = 1 (``--dist``) the all-gather strategies still issue their
+    collectives, in place, over a one-rank RCCL group, so the RCCL path runs on
+    a one-GPU box."""
     from .synthetic import WORKLOADS
 
     rank = int(os.environ.get("RANK", "0"))
@@ -643,22 +745,27 @@ def bench_distributed(args, metric: str):
     # default group gloo: barriers and the max-over-ranks reduction on the host;
     # the table all-gather runs on an RCCL group (nccl backend = RCCL on ROCm)
     os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    if "MASTER_ADDR" not in os.environ:  # plain `python bench.py --dist` (one rank)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+                          WORLD_SIZE="1")
     dist.init_process_group("gloo")
-    if world > 1 and not share:
+    force = False
+    if not share:
         exchanger = CollectiveExchange(dist.new_group(backend="nccl"))
         xname = "RCCL all_gather_into_tensor (in place, async, one per chunk)"
-    elif world > 1:
+        force = world == 1
+        if force:
+            xname += ", one-rank group (in-place self all-gather)"
+    else:
         exchanger = HostStagedExchange(None)
         xname = "gloo all-gather staged through host memory (one-GPU rehearsal)"
-    else:
-        exchanger = NoExchange()
-        xname = "none (one rank)"
-    names = [s for s in getattr(args, "dist_workloads", "reddit,arxiv").split(",") if s]
-    chunk_choices = [1, 2, 4] if world > 1 else [1]
+    names = [s for s in getattr(args, "dist_workloads", "ppi,reddit,arxiv").split(",") if s]
+    chunk_choices = [1, 2, 4] if world > 1 else [1, 2]
+    strategies = [("allgather", k) for k in chunk_choices] + [("replicate", 1)]
     work = {}
     for nm in names:
         work[nm] = _sharded_workload(WORKLOADS[nm], dev, world, rank, exchanger, args,
-                                     chunk_choices)
+                                     strategies, force_exchange=force)
     weak = None
     if not getattr(args, "no_weak", False):
         weak = _ppi_blocks_weak(WORKLOADS["ppi"], dev, world, rank, args)
@@ -666,21 +773,31 @@ def bench_distributed(args, metric: str):
     if rank == 0:
         head = work[names[0]]
         w = WORKLOADS[names[0]]
+        if head["exchange"] == "allgather":
+            par = (f"node-range partition x{world} (edge-balanced), node table all-gathered "
+                   f"in {head['chunks']} chunk(s) overlapped with the edge passes")
+        else:
+            par = (f"node-range partition x{world} (edge-balanced) of the edge work; every rank "
+                   "projects all rows (SURVEY.md §8e 'replicate': no collective in the step)")
         res = {
             "metric": metric, "value": head["value"], "unit": "edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded uniform graph of the named shape; reference-order random "
                     "init)",
-            "config": {"workload": f"{w.name}: N={head['N']} E'={head['E_prime']} "
-                                   f"Fin={w.in_channels} H={w.heads} F={w.out_channels} "
-                                   f"concat={w.concat}, one graph shared by {world} GPUs",
-                       "parallelism": f"node-range partition x{world} (edge-balanced), node "
-                                      f"table all-gathered in {head['chunks']} chunk(s) "
-                                      "overlapped with the edge passes",
+            "config": {"workload": f"{w.name}: N={head['N']} E={w.num_edges} (+N self-loops = "
+                                   f"{head['E_prime']}) Fin={w.in_channels} H={w.heads} "
+                                   f"F={w.out_channels} concat={w.concat}, one graph shared by "
+                                   f"{world} GPUs",
+                       "parallelism": par, "strategy": head["strategy"],
+                       "strategy_choice": "fastest of the strategy trials (all checked against "
+                                          "the one-GPU forward)",
                        "exchange": xname, "launch": "eager"},
             "one_gpu_same_workload": head.get("one_gpu"),
-            "workloads": work,
+            "speedup_vs_one_gpu": head.get("speedup_vs_one_gpu"),
+            "allgather": head.pop("allgather", None),
+            "workloads": {k: v for k, v in work.items() if k != names[0]},
+            "headline_detail": head,
             "ppi_blocks_data_parallel": weak,
         }
     dist.barrier()
@@ -690,3 +807,10 @@ def bench_distributed(args, metric: str):
     os.close(saved_stdout)
     if res is not None:
         print(json.dumps(res), flush=True)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]

@@ -13,9 +13,13 @@ measurement for the other single-GPU configs: Reddit scale (configs[4], the
 north-star roofline target), its power-law degree-skew variant, ogbn-arxiv
 scale (configs[3]) and the CIFAR10 superpixel batch (configs[2]).
 
-N > 1 (torchrun, one process per GPU): the north-star multi-GPU path on ONE
-shared Reddit-scale graph, node-partitioned, with the RCCL all-gather inside
-the step (atmlgraphattentionnetworks_amd/distributed.py).
+N > 1 (torchrun, one process per GPU): the same PPI-shape workload as ONE
+shared graph, node-partitioned over the GPUs, the exchange inside the step
+(the RCCL all-gather of the node table, or every rank projecting all rows,
+whichever measured faster; both reported), with Reddit and arxiv scale under
+"workloads" (atmlgraphattentionnetworks_amd/distributed.py).  The N = 1 line
+carries the per-rank compute of that partitioned step at P = 2/4/8, emulated
+on its one GPU ("multi_gpu_emulated").
 
 Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement".
 """
@@ -551,6 +555,30 @@ def reddit_cpu_sample(meas: dict, threads: int, rows: int = 1024) -> dict:
                                f"+ N self-loops = {n_edges} edges, projection over all N nodes")
 
 
+def emulated_ranks(meas: dict, ranks, exchanges=("allgather",)) -> dict:
+    """SURVEY.md §8e's compute terms, measured: the per-rank projection and
+    edge passes of the node-partitioned step at P ranks, each rank's work run
+    alone on this GPU (distributed.emulate_rank_times), plus the bytes each
+    rank would receive in the all-gather.  ``compute_only_speedup_bound`` =
+    the one-GPU step / the slowest rank's compute: what P GPUs could reach if
+    the collective were free (it is not; the N > 1 lines measure it)."""
+    from atmlgraphattentionnetworks_amd.distributed import emulate_rank_times
+    from atmlgraphattentionnetworks_amd.graph import get_csr
+    x, ei, layer = meas["_inputs"]
+    csr = get_csr(ei, x.size(0))
+    out = {}
+    with torch.no_grad():
+        for exch in exchanges:
+            for p in ranks:
+                _log(f"{meas['workload']}: emulated P={p} ({exch})")
+                r = emulate_rank_times(layer, csr, x, p, exchange=exch)
+                r["compute_only_speedup_bound"] = meas["ms_per_step"] / r["max_compute_ms"]
+                r["per_rank"] = [{k: (round(v, 5) if isinstance(v, float) else v)
+                                  for k, v in d.items()} for d in r["per_rank"]]
+                out[f"{exch}_P{p}"] = r
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -571,8 +599,11 @@ def main():
                     help="skip the training-step (forward with dropout + backward) measurement")
     ap.add_argument("--dist", action="store_true",
                     help="take the torch.distributed path even at WORLD_SIZE=1 (testing)")
-    ap.add_argument("--dist-workloads", default="reddit,arxiv",
+    ap.add_argument("--dist-workloads", default="ppi,reddit,arxiv",
                     help="multi-GPU: shared-graph workloads, the first is the headline")
+    ap.add_argument("--emulate-ranks", default="2,4,8",
+                    help="N=1: per-rank compute of the partitioned step at these rank counts, "
+                         "emulated on the one GPU ('' for none)")
     ap.add_argument("--no-weak", action="store_true",
                     help="multi-GPU: skip the data-parallel PPI-block secondary run")
     ap.add_argument("--pmc-child", default=None, help=argparse.SUPPRESS)
@@ -594,6 +625,10 @@ def main():
     head = measure_workload(args.workload, dev, args.steps, args.warmup, args.edge_iters,
                             args.graph)
     w = WORKLOADS[args.workload]
+    emu_ranks = [int(v) for v in args.emulate_ranks.split(",") if v]
+    emulated = {}
+    if emu_ranks:
+        emulated[args.workload] = emulated_ranks(head, emu_ranks, ("allgather", "replicate"))
     x, ei, layer = head["_inputs"]
     training = None if args.no_train else train_step(layer, x, ei, head["E_prime"], args.steps)
     if training is not None:
@@ -617,6 +652,9 @@ def main():
             elif nm in ("arxiv", "cifar"):
                 cpu[nm] = cpu_baseline(lw.state_dict(), xw, eiw, lw.num_heads, lw.concat,
                                        m["E_prime"], threads)
+        if emu_ranks and nm in ("arxiv", "reddit"):
+            emulated[nm] = emulated_ranks(m, emu_ranks, ("allgather", "replicate")
+                                          if nm == "arxiv" else ("allgather",))
         if nm == "reddit" and not args.no_train:
             # the training step against the eval forward
             xw, eiw, lw = m["_inputs"]
@@ -671,6 +709,12 @@ def main():
                        "hbm_frac": head["projection"]["hbm_frac"]},
         "workloads": workloads,
     }
+    if emulated:
+        result["multi_gpu_emulated"] = {
+            "what": "per-rank compute of the node-partitioned step (SURVEY.md §8e) at P ranks, "
+                    "each rank's projection and edge passes run alone on this one GPU; the "
+                    "collective is not included (bytes received per rank given instead)",
+            **emulated}
     if training is not None:
         result["training"] = training
     if cpu:

@@ -300,3 +300,27 @@ def test_table_layout_rows_and_chunks():
     assert spans[0][0] == 0 and spans[-1][1] == lay.numel
     assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
     assert lay.chunk_range(1) == (3 * lay.block_floats, 6 * lay.block_floats)
+
+
+def test_default_chunks_same_on_every_rank(monkeypatch):
+    """chunks=None: the chunk count fixes the table layout and the collectives'
+    sizes, so every rank must derive the same one even when the ranks' own
+    edge counts fall on both sides of a chunk threshold (a rank-local count
+    would make ranks issue all-gathers of different sizes: an RCCL hang)."""
+    from atmlgraphattentionnetworks_amd import distributed as D
+    x, ei, state = _case(n=300, e=6000, F=8)
+    csr = _cpu_csr(ei, x.size(0))
+    world = 3
+    bounds = D.partition_rows(csr.rowptr, world)
+    local = [int(csr.rowptr[bounds[k + 1]] - csr.rowptr[bounds[k]]) for k in range(world)]
+    # a threshold between the smallest and the largest per-rank share
+    lo, hi = min(local), max(local)
+    assert lo < hi
+    thr = (lo + hi + 1) // 2
+    monkeypatch.setattr(D, "EDGES_PER_CHUNK", thr // 2)
+    assert len({max(1, min(4, e // (thr // 2))) for e in local}) > 1  # rank-local would differ
+    layer = _Layer(state, 4, 8, True)
+    lays = [D.ShardedGAT(layer, csr, world, r, ops=CpuOps, exchanger=D.NoExchange()).layout
+            for r in range(world)]
+    assert all(lay == lays[0] for lay in lays)
+    assert lays[0].chunks == D.default_chunks(world, csr.num_edges, True)

@@ -8,10 +8,13 @@ or the single-GPU forward (full size; that forward is itself checked against
 the oracle in test_gpu_parity.py / test_gpu_fullsize.py).
 
 Bar: |sharded - ref| <= 1e-5 + 1e-5 |ref| (fp32; the passes change the
-summation order only).  RCCL itself needs distinct GPUs: the multi-process
-path is rehearsed here with two ranks on cuda:0 exchanging through gloo
-(test_bench_two_ranks_shared_gpu), and runs over RCCL in the driver's
-multi-GPU bench.
+summation order only).  RCCL with N > 1 needs distinct GPUs: the
+multi-process path is rehearsed here with two ranks on cuda:0 exchanging
+through gloo (test_bench_two_ranks_shared_gpu); the RCCL exchange itself
+(CollectiveExchange: async in-place all_gather_into_tensor per chunk, then
+wait) runs over a one-rank RCCL group (test_rccl_exchange_one_rank,
+test_bench_dist_one_rank_rccl), and over N GPUs in the driver's multi-GPU
+bench.
 """
 import pytest
 import torch
@@ -173,7 +176,7 @@ def test_bench_two_ranks_shared_gpu():
     env = dict(os.environ, GAT_BENCH_SHARE_GPU0="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--dist-workloads", "arxiv", "--steps", "6", "--warmup", "2"]
+           "--dist-workloads", "ppi,arxiv", "--steps", "6", "--warmup", "2"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
@@ -181,7 +184,103 @@ def test_bench_two_ranks_shared_gpu():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
     assert d["steps"] == 6 and d["unit"] == "edges/s"
+    assert d["config"]["workload"].startswith("ppi:")  # BASELINE.json's metric workload
+    head = d["headline_detail"]
+    assert head["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * head["check"]["max_abs_ref"]
+    assert set(head["strategy_trials_ms"]) == {"allgather_k1", "allgather_k2", "allgather_k4",
+                                               "replicate"}
+    ag = d["allgather"] if d["allgather"] is not None else head
+    assert ag["exchange"] == "allgather" and ag["collective_bytes_received_per_rank"] > 0
+    assert ag["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * ag["check"]["max_abs_ref"]
+    assert d["speedup_vs_one_gpu"] > 0 and d["one_gpu_same_workload"]["value"] > 0
     arx = d["workloads"]["arxiv"]
     assert arx["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * arx["check"]["max_abs_ref"]
-    assert set(arx["chunk_trials_ms"]) == {"1", "2", "4"} or set(arx["chunk_trials_ms"]) == {1, 2, 4}
     assert d["ppi_blocks_data_parallel"]["value"] > 0
+
+
+_RCCL_ONE_RANK = r"""
+import json, os, sys
+sys.path.insert(0, os.getcwd())
+import torch, torch.distributed as dist
+from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
+from atmlgraphattentionnetworks_amd.distributed import CollectiveExchange, ShardedGAT
+from atmlgraphattentionnetworks_amd.synthetic import uniform_graph
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
+torch.manual_seed(0)
+layer = GraphAttentionLayer(50, 8, num_heads=8, concat=True).to(dev).eval()
+with torch.no_grad():
+    layer.bias.normal_()
+x = torch.randn(3000, 50, device=dev)
+ei = uniform_graph(3000, 60000, seed=4, device=dev)
+csr = get_csr(ei, 3000)
+res = {}
+with torch.no_grad():
+    one = layer(x, ei)
+    for k in (1, 3):
+        ex = CollectiveExchange(None)
+        sh = ShardedGAT(layer, csr, 1, 0, chunks=k, exchanger=ex, force_exchange=True)
+        hs = []
+        xl = sh.local_x(x)
+        for c in range(sh.chunks):
+            sh.project_chunk(xl, c)
+            hs.append(sh.exchange_start(c))
+        assert all(h is not None for h in hs), "exchange_start short-circuited"
+        for c in range(sh.chunks):
+            sh.exchanger.wait(hs[c])
+            sh.edge_pass(c)
+        torch.cuda.synchronize()
+        res[k] = float((sh.out - one).abs().max())
+        res[f"chunks{k}"] = sh.chunks
+        res[f"scale{k}"] = float(one.abs().max())
+dist.destroy_process_group()
+print(json.dumps(res))
+"""
+
+
+def test_rccl_exchange_one_rank():
+    """CollectiveExchange over a real RCCL communicator (one rank: the GPU box
+    has one GPU): ``new`` nccl process group, the asynchronous in-place
+    all_gather_into_tensor of each table chunk, ``wait()`` ordering the edge
+    passes after it on torch's stream — with 1 and 3 chunks.  The output must
+    equal the single-GPU forward."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _RCCL_ONE_RANK], cwd=root, capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("1", "3"):
+        assert d[f"chunks{k}"] == int(k)
+        assert d[k] <= 1e-5 + 1e-5 * d[f"scale{k}"], d
+
+
+def test_bench_dist_one_rank_rccl():
+    """``bench.py --dist`` at one rank (no torchrun): the multi-GPU bench path
+    with its all-gather strategies issued over a one-rank RCCL group, the
+    PPI-shape headline, and the check against the one-GPU forward."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--dist", "--dist-workloads", "ppi",
+                        "--no-weak", "--steps", "6", "--warmup", "2"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["config"]["workload"].startswith("ppi:")
+    assert "RCCL" in d["config"]["exchange"]
+    head = d["headline_detail"]
+    assert set(head["strategy_trials_ms"]) == {"allgather_k1", "allgather_k2", "replicate"}
+    ag = d["allgather"] if d["allgather"] is not None else head
+    assert ag["collective_ms"] > 0
+    assert ag["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * ag["check"]["max_abs_ref"]
