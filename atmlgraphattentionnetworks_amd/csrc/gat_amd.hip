@@ -372,6 +372,38 @@ __device__ __forceinline__ float group_sum16(float v, int w) {
 }
 
 // ---------------------------------------------------------------------------
+// Write-through (sc1) stores for a kernel's final outputs.  The bytes go to
+// memory as they are stored, so the kernel ends with no dirty L2 lines: the
+// dependent kernel's start does not wait for an L2 write-back of them
+// (MI355X_MICROARCH.md, persistent-kernel price list, row 'boundary':
+// + B / 6 TB/s for B dirty bytes left by the predecessor).  Buffer stores from
+// a wave-uniform base (a kernel argument) with 32-bit byte offsets; an element
+// past 2 GiB from the base takes a plain store.
+// ---------------------------------------------------------------------------
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr size_t kWtMaxOff = 0x7FFFFFF0u;
+
+__device__ __forceinline__ void store_out4(float* base, size_t idx, f32x4 v, int wt) {
+    const size_t off = idx * sizeof(float);
+    if (wt && off < kWtMaxOff) {
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, (int)off, 0, 16);
+    } else {
+        *reinterpret_cast<f32x4*>(base + idx) = v;
+    }
+}
+
+__device__ __forceinline__ void store_out1(float* base, size_t idx, float v, int wt) {
+    const size_t off = idx * sizeof(float);
+    if (wt && off < kWtMaxOff) {
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 16);
+    } else {
+        base[idx] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Projection, software-pipelined K loop (Fin > 64).  fp32 MFMA throughput
 // (157 TF) bounds a [N, Fin] x [Fin, 64] projection at large Fin (Reddit:
 // 18 GFLOP -> 115 us).
@@ -598,7 +630,7 @@ __global__ __launch_bounds__(256) void k_project_x3(
     const float* __restrict__ a1, const float* __restrict__ c1,
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
-    float* __restrict__ s_dst, int slice_w, long long slice_stride) {
+    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt) {
     // RG 16-row groups per wave, 4 waves: BM = 64 RG rows per block
     constexpr int BK = 64, BN = NT * 16, NTH = 256, BM = 64 * RG;
     constexpr int XS = BK + 4, WSB = BK + 8, OS = BN + 4;
@@ -774,8 +806,8 @@ __global__ __launch_bounds__(256) void k_project_x3(
                 const float v2 = li == 0 ? p2[0] : li == 1 ? p2[1] : li == 2 ? p2[2] : p2[3];
                 const int rr = row0 + 16 * g + kq * 4 + li;
                 if (rr < n) {
-                    if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = v1 + c1[h];
-                    s_dst[(size_t)rr * H + h] = v2 + c2[h];
+                    if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, v1 + c1[h], store_wt);
+                    store_out1(s_dst, (size_t)rr * H + h, v2 + c2[h], store_wt);
                 }
             }
             if (F < 4 && li == 0 && h < H) {  // heads narrower than 4 lanes: rows F..3
@@ -783,8 +815,8 @@ __global__ __launch_bounds__(256) void k_project_x3(
                 for (int i = 1; i < 4; ++i) {
                     const int rr = row0 + 16 * g + kq * 4 + i;
                     if (i >= F && rr < n) {
-                        if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
-                        s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
+                        if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, p1[i] + c1[h], store_wt);
+                        store_out1(s_dst, (size_t)rr * H + h, p2[i] + c2[h], store_wt);
                     }
                 }
             }
@@ -796,11 +828,11 @@ __global__ __launch_bounds__(256) void k_project_x3(
     const int col = 4 * (tid % C4);
     if (col < hfp) {
         const int g = col / slice_w;
-        float* dst = Wh + (size_t)g * (size_t)slice_stride + (col - g * slice_w);
+        const size_t base = (size_t)g * (size_t)slice_stride + (col - g * slice_w);
         const int rows = min(BM, n - blk0);
         for (int r = tid / C4; r < rows; r += NTH / C4)
-            *reinterpret_cast<f32x4*>(dst + (size_t)(blk0 + r) * ld_wh) =
-                *reinterpret_cast<const f32x4*>(Os + r * OS + col);
+            store_out4(Wh, base + (size_t)(blk0 + r) * ld_wh,
+                       *reinterpret_cast<const f32x4*>(Os + r * OS + col), store_wt);
     }
 }
 
@@ -828,7 +860,7 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
     const float* __restrict__ a1, const float* __restrict__ c1,
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
-    float* __restrict__ s_dst, int slice_w, long long slice_stride) {
+    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt) {
     constexpr int BN = NT * 16, KP = KS * 32;  // padded K
     constexpr int WSB = KP + 8, OS = BN + 4;
     constexpr int NL = 8 / LW;                  // loads per 8-float fragment
@@ -979,8 +1011,8 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
                 const float v2 = li == 0 ? p2[0] : li == 1 ? p2[1] : li == 2 ? p2[2] : p2[3];
                 const int rr = row0 + kq * 4 + li;
                 if (rr < n) {
-                    if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = v1 + cs1[t];
-                    s_dst[(size_t)rr * H + h] = v2 + cs2[t];
+                    if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, v1 + cs1[t], store_wt);
+                    store_out1(s_dst, (size_t)rr * H + h, v2 + cs2[t], store_wt);
                 }
             }
             if (F < 4 && li == 0 && h < H) {  // heads narrower than 4 lanes: rows F..3
@@ -988,8 +1020,9 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
                 for (int i = 1; i < 4; ++i) {
                     const int rr = row0 + kq * 4 + i;
                     if (i >= F && rr < n) {
-                        if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + cs1[t];
-                        s_dst[(size_t)rr * H + h] = p2[i] + cs2[t];
+                        if (Ss != nullptr)
+                            store_out1(Ss, (size_t)rr * ld_s + h, p1[i] + cs1[t], store_wt);
+                        store_out1(s_dst, (size_t)rr * H + h, p2[i] + cs2[t], store_wt);
                     }
                 }
             }
@@ -1002,9 +1035,9 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
             const int r = idx / C4, col = 4 * (idx % C4);
             if (col < hfp && row0 + r < n) {
                 const int g = col / slice_w;
-                *reinterpret_cast<f32x4*>(Wh + (size_t)g * (size_t)slice_stride +
-                                          (size_t)(row0 + r) * ld_wh + (col - g * slice_w)) =
-                    *reinterpret_cast<const f32x4*>(Os + r * OS + col);
+                store_out4(Wh, (size_t)g * (size_t)slice_stride + (size_t)(row0 + r) * ld_wh +
+                                   (col - g * slice_w),
+                           *reinterpret_cast<const f32x4*>(Os + r * OS + col), store_wt);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1041,7 +1074,7 @@ __global__ __launch_bounds__(256) void k_project_wk(
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ Wh, int ld_wh,
     float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst,
-    int slice_w, long long slice_stride) {
+    int slice_w, long long slice_stride, int store_wt) {
     constexpr int BM = 64, BN = NT * 16;
     constexpr int OS = BN + 4;  // output-tile stride: float4-aligned rows, no write conflicts
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1167,8 +1200,8 @@ __global__ __launch_bounds__(256) void k_project_wk(
             if (4 * c4 + 2 >= HF) v.z = 0.f;
             if (4 * c4 + 3 >= HF) v.w = 0.f;
         }
-        *reinterpret_cast<f32x4*>(Wh + (size_t)g * (size_t)slice_stride +
-                                  (size_t)(row0 + r) * ld_wh + 4 * q) = v;
+        store_out4(Wh, (size_t)g * (size_t)slice_stride + (size_t)(row0 + r) * ld_wh + 4 * q, v,
+                   store_wt);
     }
     // attention Linears on the fp32 Wh (GAT.py:44-45): s = Wh_h . a_h + c_h
     for (int idx = tid; idx < rows * H; idx += 256) {
@@ -1181,8 +1214,8 @@ __global__ __launch_bounds__(256) void k_project_wk(
             v1 = fmaf(o[f], p1[f], v1);
             v2 = fmaf(o[f], p2[f], v2);
         }
-        if (Ss != nullptr) Ss[(size_t)(row0 + r) * ld_s + h] = v1 + c1s[h];
-        s_dst[(size_t)(row0 + r) * H + h] = v2 + c2s[h];
+        if (Ss != nullptr) store_out1(Ss, (size_t)(row0 + r) * ld_s + h, v1 + c1s[h], store_wt);
+        store_out1(s_dst, (size_t)(row0 + r) * H + h, v2 + c2s[h], store_wt);
     }
 }
 
@@ -1420,7 +1453,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const float* __restrict__ bias, float* __restrict__ out, int ld_out,
     float* __restrict__ lse, DropArgs drop_arg, float* __restrict__ y_heads,
     int nslices, int slice_w, long long slice_stride, float* __restrict__ q_heads,
-    float* __restrict__ r_heads) {
+    float* __restrict__ r_heads, int store_wt) {
     const DropArgs drop = resolve_drop(drop_arg);
     // col values held per lane per chunk.  Groups of >= 4 lanes: every quad of
     // the group holds the chunk's indices (lane c: edges (c & 3) + 4t), so the
@@ -1470,10 +1503,12 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     // rows of >= 1024 edges keep Kahan-compensated running sums (lc, cmp) over
     // per-chunk partial sums: a 10k-edge hub row otherwise accumulates more fp32
     // error than the reference's own.  Shorter rows add directly (cheaper).
-    f32x4 acc[V], cmp[V], accq[V];
-    float lc = 0.f, racc = 0.f;
+    // (the kink sums Q, R get the same compensation on those rows: the backward
+    // forms ds_dst = dy.Q - delta R, a difference of two large sums)
+    f32x4 acc[V], cmp[V], accq[V], cmpq[V];
+    float lc = 0.f, racc = 0.f, rc = 0.f;
 #pragma unroll
-    for (int q = 0; q < V; ++q) acc[q] = cmp[q] = accq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < V; ++q) acc[q] = cmp[q] = accq[q] = cmpq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (er.load) {  // continue a row whose earlier segments a previous pass ran
         m = er.st_ml[(size_t)si * 2 * H + h];
         l = er.st_ml[(size_t)si * 2 * H + H + h];
@@ -1562,14 +1597,15 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
             for (int q = 0; q < V; ++q) accq[q] *= scale;
         }
-        // kink sums of one edge (s[u] = LReLU(z) log2e has the sign of z)
-        auto kink = [&](int u, float p, float pa) {
+        // kink sums of one edge (s[u] = LReLU(z) log2e has the sign of z), into
+        // (rr, qq): the running sums, or a Kahan row's chunk partials
+        auto kink = [&](int u, float p, float pa, float& rr, f32x4 (&qq)[V]) {
             if constexpr (KINK) {
                 const float lk = s[u] > 0.f ? 1.f : slope;
-                racc += p * lk;
+                rr += p * lk;
                 const float pq = pa * lk;
 #pragma unroll
-                for (int q = 0; q < V; ++q) accq[q] += pq * v[u][q];
+                for (int q = 0; q < V; ++q) qq[q] += pq * v[u][q];
             }
         };
         if (!kahan) {
@@ -1581,16 +1617,21 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 if (dropping) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
                 for (int q = 0; q < V; ++q) acc[q] += pa * v[u][q];
-                kink(u, p, pa);
+                kink(u, p, pa, racc, accq);
             }
         } else {
             lc *= scale;
 #pragma unroll
             for (int q = 0; q < V; ++q) cmp[q] *= scale;
-            float ls = 0.f;
-            f32x4 cs[V];
+            float ls = 0.f, rs = 0.f;
+            f32x4 cs[V], qs[V];
 #pragma unroll
-            for (int q = 0; q < V; ++q) cs[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < V; ++q) cs[q] = qs[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (KINK) {
+                rc *= scale;
+#pragma unroll
+                for (int q = 0; q < V; ++q) cmpq[q] *= scale;
+            }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
@@ -1599,19 +1640,28 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 if (dropping) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
                 for (int q = 0; q < V; ++q) cs[q] += pa * v[u][q];
-                kink(u, p, pa);
+                kink(u, p, pa, rs, qs);
             }
             // Kahan: add the chunk sums into the running sums
-            const float y = ls - lc;
-            const float t = l + y;
-            lc = (t - l) - y;
-            l = t;
+            auto kahan_add = [](float& sum, float& c, float part) {
+                const float y = part - c;
+                const float t = sum + y;
+                c = (t - sum) - y;
+                sum = t;
+            };
+            auto kahan_add4 = [](f32x4& sum, f32x4& c, f32x4 part) {
+                const f32x4 y = part - c;
+                const f32x4 t = sum + y;
+                c = (t - sum) - y;
+                sum = t;
+            };
+            kahan_add(l, lc, ls);
 #pragma unroll
-            for (int q = 0; q < V; ++q) {
-                const f32x4 yq = cs[q] - cmp[q];
-                const f32x4 tq = acc[q] + yq;
-                cmp[q] = (tq - acc[q]) - yq;
-                acc[q] = tq;
+            for (int q = 0; q < V; ++q) kahan_add4(acc[q], cmp[q], cs[q]);
+            if constexpr (KINK) {
+                kahan_add(racc, rc, rs);
+#pragma unroll
+                for (int q = 0; q < V; ++q) kahan_add4(accq[q], cmpq[q], qs[q]);
             }
         }
         m = m_new;
@@ -1681,8 +1731,9 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         if (c_ok) {
 #pragma unroll
             for (int q = 0; q < V; ++q)
-                *reinterpret_cast<f32x4*>(q_heads + (size_t)r * HF + coff + 4 * q) = accq[q] * inv;
-            if ((coff % F) == 0) r_heads[(size_t)r * H + h] = racc * inv;
+                *reinterpret_cast<f32x4*>(q_heads + (size_t)r * HF + coff + 4 * q) =
+                    (kahan ? accq[q] - cmpq[q] : accq[q]) * inv;
+            if ((coff % F) == 0) r_heads[(size_t)r * H + h] = (kahan ? racc - rc : racc) * inv;
         }
     }
     if (concat) {
@@ -1690,7 +1741,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
             for (int q = 0; q < V; ++q) {
                 const f32x4 b = *reinterpret_cast<const f32x4*>(bias + coff + 4 * q);
-                *reinterpret_cast<f32x4*>(out + (size_t)r * ld_out + coff + 4 * q) = acc[q] * inv + b;
+                store_out4(out, (size_t)r * ld_out + coff + 4 * q, acc[q] * inv + b, store_wt);
             }
         }
     } else {
@@ -1713,11 +1764,11 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
             for (int q = 0; q < V; ++q) {
                 const int f0 = 4 * V * c + 4 * q;
-                float* o = out + (size_t)r * ld_out + f0;
-                o[0] = y[q].x / hh + bias[f0 + 0];
-                o[1] = y[q].y / hh + bias[f0 + 1];
-                o[2] = y[q].z / hh + bias[f0 + 2];
-                o[3] = y[q].w / hh + bias[f0 + 3];
+                const size_t o = (size_t)r * ld_out + f0;
+                store_out1(out, o + 0, y[q].x / hh + bias[f0 + 0], store_wt);
+                store_out1(out, o + 1, y[q].y / hh + bias[f0 + 1], store_wt);
+                store_out1(out, o + 2, y[q].z / hh + bias[f0 + 2], store_wt);
+                store_out1(out, o + 3, y[q].w / hh + bias[f0 + 3], store_wt);
             }
         }
     }
@@ -2702,7 +2753,7 @@ const char* const kKnobNames[] = {
     "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
     "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
     "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS", "GAT_BWD_KINK",
-    "GAT_WGRAD_LW"};
+    "GAT_WGRAD_LW",    "GAT_STORE_WT"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -2730,6 +2781,12 @@ const char* knob(const char* name) {
     for (int i = 0; i < kNumKnobs; ++i)
         if (std::strcmp(kKnobNames[i], name) == 0) return g_knobs.set[i] ? g_knobs.val[i] : nullptr;
     return nullptr;
+}
+
+// GAT_STORE_WT (A/B knob): 1 = final outputs stored write-through (sc1), 0 = plain
+int store_wt_on() {
+    const char* v = knob("GAT_STORE_WT");
+    return v != nullptr ? (std::atoi(v) != 0) : 1;
 }
 
 bool kernel_choice(const char* env, const char* slow) {
@@ -2783,6 +2840,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((n + 63) / 64), block(256);
     const int nt = (hf + 15) / 16;
+    const int store_wt = store_wt_on();  // Wh / scores stored write-through
     // GAT_PROJ_KERNEL (A/B knob, tools/tests): "wk" (whole K in LDS; the
     // default for fin <= 64), "pipe" (pipelined K loop; the default for larger
     // fin), "tiled" / "lds" (K-tiled fallback, shuffle / LDS epilogue)
@@ -2812,7 +2870,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #define GAT_WRES(NTV, LWV, KSV)                                                               \
     hipLaunchKernelGGL((k_project_wres<NTV, LWV, KSV>), dim3(grid_w), dim3(256), 0, st, x, n, \
                        fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src,  \
-                       ld_s, s_dst, slice_w, slice_stride)
+                       ld_s, s_dst, slice_w, slice_stride, store_wt)
 #define GAT_WRES_KS(NTV, LWV)                                          \
     switch (ks) {                                                      \
         case 1: GAT_WRES(NTV, LWV, 1); break;                          \
@@ -2840,7 +2898,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     case NT:                                                                                  \
         hipLaunchKernelGGL((k_project_wk<NT>), grid, block, wk_lds, st, x, n, fin, w, b,      \
                            a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s,  \
-                           s_dst, slice_w, slice_stride);                                     \
+                           s_dst, slice_w, slice_stride, store_wt);                           \
         break;
         switch (nt) {
             GAT_WK_CASE(1) GAT_WK_CASE(2) GAT_WK_CASE(3) GAT_WK_CASE(4)
@@ -2865,7 +2923,9 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         // split-bf16 matrix cores (k_project_x3) unless GAT_PROJ_X3=0 (A/B knob:
         // the fp32-MFMA k_project_pipe2)
         bool x3 = true;
+#ifdef GAT_AB_KERNELS
         if (const char* v = knob("GAT_PROJ_X3")) x3 = std::atoi(v) != 0;
+#endif
         // rows per block (GAT_PROJ_BM A/B knob: 64 = one 16-row group per wave,
         // 128 = two, sharing every B fragment)
         // tools/proj_ab.py: 4-float x rows (arxiv) prefer 64 rows per block with two
@@ -2873,20 +2933,26 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         // fragments with one chunk in flight
         int bm = lw == 4 ? 64 : 128;
         if (const char* v = knob("GAT_PROJ_BM")) bm = std::atoi(v);
+#ifdef GAT_AB_KERNELS
+#define GAT_PIPE2_FP32(NT, LWV)                                                                \
+        hipLaunchKernelGGL((k_project_pipe2<NT, LWV>), gp, bp, 0, st, x, n, fin, w, b, a_src, \
+                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
+                           slice_w, slice_stride)
+#else
+#define GAT_PIPE2_FP32(NT, LWV) (void)gp
+#endif
 #define GAT_PIPE2(NT, LWV)                                                                     \
     if (x3 && bm == 128)                                                                       \
         hipLaunchKernelGGL((k_project_x3<NT, LWV, 2, 1>), dim3((n + 127) / 128), bp, 0, st,    \
                            x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,     \
-                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride);                 \
+                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt);       \
     else if (x3)                                                                               \
         hipLaunchKernelGGL((k_project_x3<NT, LWV, 1, 2>), dim3((n + 63) / 64), bp, 0, st, x, n, \
                            fin, w, b, a_src,                                                  \
                            c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
-                           slice_w, slice_stride);                                            \
+                           slice_w, slice_stride, store_wt);                                  \
     else                                                                                       \
-        hipLaunchKernelGGL((k_project_pipe2<NT, LWV>), gp, bp, 0, st, x, n, fin, w, b, a_src, \
-                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
-                           slice_w, slice_stride)
+        GAT_PIPE2_FP32(NT, LWV)
 #define GAT_PIPE2_LW(NT)                                  \
     if (lw == 4) { GAT_PIPE2(NT, 4); }                    \
     else if (lw == 2) { GAT_PIPE2(NT, 2); }               \
@@ -2896,6 +2962,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         else { GAT_PIPE2_LW(4) }
 #undef GAT_PIPE2_LW
 #undef GAT_PIPE2
+#undef GAT_PIPE2_FP32
         return status_of(hipGetLastError());
     }
     if (sliced) return GAT_EUNSUPPORTED;  // the kernels below write row-major Wh only
@@ -2952,7 +3019,9 @@ static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A
     // kernel — caps the blocks resident per CU (160 KB / bytes)
     size_t lds = 0;
     if (const char* el = knob("GAT_EDGE_LDS")) lds = (size_t)std::atol(el);
-    if constexpr ((V == 1 && (U == 4 || U == 8)) || (V == 2 && (U == 8 || U == 16))) {
+    // the pipelined form is instantiated for the pair the default schedule
+    // pipelines (U = 16, V = 2: Reddit-scale rows); elsewhere the knob is ignored
+    if constexpr (V == 2 && U == 16) {
         if (pipe) {
             hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true, KINK>), grid, block, lds, st, a...);
             return;
@@ -3000,6 +3069,9 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         return GAT_EINVAL;
     }
     const int slice_w = sliced ? ld_wh : round_up4(hf);
+    // write-through output stores: only for the final (eval) output, which the
+    // next kernel reads, not for the training forward's extra tensors
+    const int store_wt = (lse == nullptr && q_heads == nullptr) ? store_wt_on() : 0;
     if (s_src != nullptr && ld_s < heads) return GAT_EINVAL;
     const bool have_a = a_src != nullptr && c_src != nullptr;
     if (s_src == nullptr && !have_a) return GAT_EINVAL;
@@ -3023,8 +3095,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     edges_per_row_hint &= ~GAT_HINT_LOCAL;
     int vv = edges_per_row_hint >= 128 ? 2 : 1;
     if (local_hint && !sliced && round_up4(hf) <= 32) vv = 2;
-    if (const char* ev = knob("GAT_EDGE_V")) vv = std::atoi(ev);
-    if (vv != 1 && vv != 2 && vv != 4) vv = 1;
+    if (const char* ev = knob("GAT_EDGE_V")) vv = std::atoi(ev) >= 2 ? 2 : 1;
 
     while (vv > 1 && f % (4 * vv) != 0) vv >>= 1;
     const int hl = f / (4 * vv);  // lanes per head
@@ -3063,7 +3134,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
 #define GAT_GRP_KARGS                                                                         \
     er, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,   \
         heads, f, hf, concat, negative_slope, bias, out, ld_out, lse, drop, y_heads, nslices,  \
-        slice_w, slice_stride, q_heads, r_heads
+        slice_w, slice_stride, q_heads, r_heads, store_wt
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
     if (kink)                                                                         \
         launch_edge_kink<G, UU, VV>(pipe, grid, block, st, GAT_GRP_KARGS);             \
@@ -3075,21 +3146,27 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     if (u == 4) { GAT_GRP_LAUNCH(G, 4, VV); }                                         \
     else if (u == 16) { GAT_GRP_LAUNCH(G, 16, VV); }                                  \
     else { GAT_GRP_LAUNCH(G, 8, VV); }
-#define GAT_GRP_G(VV)                                 \
-    switch (g) {                                      \
+#define GAT_GRP_G32(VV)                               \
         case 1: GAT_GRP_U(1, VV) break;               \
         case 2: GAT_GRP_U(2, VV) break;               \
         case 4: GAT_GRP_U(4, VV) break;               \
         case 8: GAT_GRP_U(8, VV) break;               \
         case 16: GAT_GRP_U(16, VV) break;             \
-        case 32: GAT_GRP_U(32, VV) break;             \
-        case 64: GAT_GRP_U(64, VV) break;             \
-        default: return GAT_EUNSUPPORTED;             \
-    }
-        if (vv == 4) { GAT_GRP_G(4) }
-        else if (vv == 2) { GAT_GRP_G(2) }
-        else { GAT_GRP_G(1) }
-#undef GAT_GRP_G
+        case 32: GAT_GRP_U(32, VV) break;
+        // V = 2 owns <= 256 / 8 = 32 lanes per row: no G = 64 instance
+        if (vv == 2) {
+            switch (g) {
+                GAT_GRP_G32(2)
+                default: return GAT_EUNSUPPORTED;
+            }
+        } else {
+            switch (g) {
+                GAT_GRP_G32(1)
+                case 64: GAT_GRP_U(64, 1) break;
+                default: return GAT_EUNSUPPORTED;
+            }
+        }
+#undef GAT_GRP_G32
 #undef GAT_GRP_U
 #undef GAT_GRP_LAUNCH
 #undef GAT_GRP_KARGS

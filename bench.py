@@ -539,10 +539,10 @@ def train_step(layer, x, ei, n_edges: int, steps: int) -> dict:
 
 
 def reddit_cpu_sample(meas: dict, threads: int, rows: int = 1024) -> dict:
-    """CPU baseline at Reddit scale on a bounded sample: the oracle over the
-    complete in-edge sets of `rows` random target rows (the full forward
-    materialises ~90 GB of edge tensors on the host).  The oracle still
-    projects all N nodes and adds all N self-loops."""
+    """CPU baseline at Reddit scale (uniform or power-law) on a bounded
+    sample: the oracle over the complete in-edge sets of `rows` random target
+    rows (the full forward materialises ~90 GB of edge tensors on the host).
+    The oracle still projects all N nodes and adds all N self-loops."""
     x, ei, layer = meas["_inputs"]
     g = torch.Generator(device="cpu")
     g.manual_seed(7)
@@ -591,7 +591,7 @@ def main():
                          "GPU time, and graph replays add a ~9 us gap each)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--edge-iters", type=int, default=20)
-    ap.add_argument("--workloads", default="reddit,reddit_powerlaw,arxiv,cifar",
+    ap.add_argument("--workloads", default="reddit,reddit_powerlaw,arxiv,cifar,cifar_h8",
                     help="extra single-GPU workloads reported under 'workloads' ('' for none)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 --pmc passes (traffic, L2 hit, MFMA busy)")
@@ -647,9 +647,9 @@ def main():
         if not args.no_cpu_baseline:
             _log(f"cpu baseline {nm}")
             xw, eiw, lw = m["_inputs"]
-            if nm == "reddit":
+            if nm in ("reddit", "reddit_powerlaw"):
                 cpu[nm] = reddit_cpu_sample(m, threads)
-            elif nm in ("arxiv", "cifar"):
+            else:
                 cpu[nm] = cpu_baseline(lw.state_dict(), xw, eiw, lw.num_heads, lw.concat,
                                        m["E_prime"], threads)
         if emu_ranks and nm in ("arxiv", "reddit"):
@@ -666,7 +666,7 @@ def main():
         torch.cuda.empty_cache()
     traffic = {}
     if not args.no_pmc:
-        names = [args.workload] + [nm for nm in ("reddit", "reddit_powerlaw") if nm in extra]
+        names = [args.workload] + extra
         traffic = pmc_traffic(names, os.path.join(ROOT, "gpurun_out", "bench_pmc"))
     head_sum = _workload_summary(head, traffic.get(args.workload))
     workloads = {nm: _workload_summary(m, traffic.get(nm)) for nm, m in measured.items()}

@@ -84,6 +84,10 @@ int gat_table_layout(int heads, int f, int* ld, int* s_off);
  *                      zeroed; ld_wh % 4 == 0, ld_wh >= round_up(heads*f, 4)
  *   s_src  [n, ld_s]   Wh_h . a_src_h + c_src_h   (ld_s >= heads)
  *   s_dst  [n, heads]  Wh_h . a_dst_h + c_dst_h
+ * Non-finite inputs: a row of x holding +/-Inf or NaN affects that row only;
+ * every output the fp32 reference makes non-finite is non-finite here too, but
+ * where the reference gives +/-Inf the split-bf16 kernels (fin > 64) may give
+ * NaN (the exact bf16 split of an infinity is not defined).
  */
 int gat_project(const float* x, int n, int fin, const float* w, const float* b,
                 const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,

@@ -22,32 +22,29 @@ def dev():
     return torch.device("cuda", 0)
 
 
-# Every parity case runs on the specialised kernels (the default wherever the
-# shape allows) AND on the generic kernels, selected by the library's env knobs.
+# Every parity case runs on the default kernels AND on one representative of
+# each other kernel family the library can dispatch to (selected by its env
+# knobs): the product paths a shape or a graph can take, not every knob value.
 VARIANTS = {
     "fast": {},
-    "proj_wk": {"GAT_PROJ_WRES": "0"},  # whole-K fp32 / K-chunked projections
-    "proj_wres": {"GAT_PROJ_WRES": "1"},  # W-resident split-bf16 for every fin <= 128
-    "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds"},
-    "fast_u4": {"GAT_EDGE_U": "4"},
-    "fast_u16": {"GAT_EDGE_U": "16"},
+    # edge kernel: chunk length by hint (U = 8, 16), two float4s per lane, the
+    # pipelined Reddit-scale kernel, the gathered-s_src form, the generic one
+    "u8": {"GAT_EDGE_U": "8"},
+    "u16": {"GAT_EDGE_U": "16"},
+    "v2_natural": {"GAT_EDGE_V": "2", "GAT_EDGE_ORDER": "natural"},
+    "pipe_u16_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
     "gather_score": {"GAT_EDGE_SCORE": "gather"},
+    "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds"},
+    # projection: k_project_x3 for 64 < fin <= 128 (WRES=0), k_project_wres for
+    # every fin <= 128, the tiled fallback; plain stores instead of write-through
+    "proj_wk": {"GAT_PROJ_WRES": "0"},
+    "proj_wres": {"GAT_PROJ_WRES": "1"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
-    "proj_pipe": {"GAT_PROJ_KERNEL": "pipe"},  # split-bf16 MFMA (k_project_x3)
-    "proj_pipe_fp32": {"GAT_PROJ_KERNEL": "pipe", "GAT_PROJ_X3": "0"},  # fp32 MFMA
-    "v2": {"GAT_EDGE_V": "2"},
-    "v4_natural": {"GAT_EDGE_V": "4", "GAT_EDGE_ORDER": "natural"},
+    "plain_stores": {"GAT_STORE_WT": "0"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
-    "sliced4_u16": {"GAT_WH_SLICES": "4", "GAT_EDGE_U": "16"},
-    "sliced8": {"GAT_WH_SLICES": "8"},
     "sliced8_v2": {"GAT_WH_SLICES": "8", "GAT_EDGE_V": "2"},
     "sliced4_proj_pipe": {"GAT_WH_SLICES": "4", "GAT_PROJ_WK_MAX": "0"},
-    # gathers pipelined one chunk ahead (default for U = 16, V = 2 only)
-    "pipe_u4": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "4"},
-    "pipe_u8_sliced2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "8", "GAT_WH_SLICES": "2"},
-    "pipe_u16_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
-    "nopipe_u16_v2": {"GAT_EDGE_PIPE": "0", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
 }
 
 
@@ -55,7 +52,7 @@ VARIANTS = {
 def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
-              "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_X3", "GAT_PROJ_WRES",
+              "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
@@ -321,3 +318,41 @@ def test_sliced_default_with_unaligned_x_view():
                                 pp.c_dst.data_ptr(), H, F, 2, wh.data_ptr(), n, None, H,
                                 sd.data_ptr(), torch.cuda.current_stream().cuda_stream)
     assert rc == _lib.GAT_EUNSUPPORTED
+
+
+@pytest.mark.parametrize("fin", [50, 128, 200])
+def test_projection_non_finite_inputs(fin):
+    """Contract for non-finite x (include/gat_amd.h, gat_project): rows
+    without a non-finite value are unaffected (no leak into other rows through
+    clamped or padded loads), and every Wh / s_dst entry the fp64 reference
+    makes non-finite is non-finite here too (the split-bf16 kernels, fin > 64,
+    give NaN where the reference gives +/-Inf: Inf - bf16(Inf) is NaN)."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    from atmlgraphattentionnetworks_amd.layer import alloc_table, project
+    d = dev()
+    torch.manual_seed(0)
+    H, F, n = 8, 8, 700
+    layer = GraphAttentionLayer(fin, F, num_heads=H, concat=True).to(d).eval()
+    x = torch.randn(n, fin, device=d)
+    clean = x.clone()
+    bad_rows = [0, 17, 351, n - 1]
+    x[0, 3] = float("inf")
+    x[17, fin - 1] = float("-inf")
+    x[351, fin // 2] = float("nan")
+    x[n - 1, 0] = float("inf")
+    pp = layer.packed()
+    with torch.no_grad():
+        t_bad, sd_bad = project(x, pp, H, F, table=alloc_table(n, H, F, d))
+        t_ok, sd_ok = project(clean, pp, H, F, table=alloc_table(n, H, F, d))
+    good = torch.ones(n, dtype=torch.bool, device=d)
+    good[bad_rows] = False
+    assert torch.equal(t_bad.wh[good], t_ok.wh[good])
+    assert torch.equal(sd_bad[good], sd_ok[good])
+    w64 = pp.w.double()
+    ref = x.double() @ w64.T + pp.b.double()
+    ours = t_bad.wh[:, :H * F]
+    for r in bad_rows:
+        nf = ~torch.isfinite(ref[r])
+        assert bool(nf.any())
+        assert not bool(torch.isfinite(ours[r][nf]).any()), (r, ours[r])
+        assert not bool(torch.isfinite(sd_bad[r]).any())
