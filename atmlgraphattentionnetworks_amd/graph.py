@@ -160,6 +160,60 @@ def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
                    torch.cat([ve, rp[rest + 1]]).to(i32).contiguous())
 
 
+class SchedCSR(NamedTuple):
+    """The CSR's ``col`` re-laid out in the eval edge kernel's row schedule
+    (``order``, rows by descending in-degree): schedule position p's in-edges
+    are ``col[b[p]:e[p]]``, adjacent to position p+1's.  A lane group then
+    reads its row bounds in one load that does not wait for ``order[p]``, and
+    the rows sharing a wave read one contiguous run of ``col``.  Built for
+    short-row graphs only (``sched_csr``): there the row prologue's chain of
+    dependent loads (order -> rowptr -> col -> Wh) is a large part of a
+    wave's life."""
+    b: torch.Tensor  # int32 [N]
+    e: torch.Tensor  # int32 [N]
+    col: torch.Tensor  # int32 [E']
+
+
+SCHED_MAX_EPR = 64  # scheduled copy below this many in-edges per row (E'/N)
+
+
+def build_sched_csr(csr: "CSRGraph") -> SchedCSR:
+    rp = csr.rowptr.to(torch.int64)
+    order = csr.order.to(torch.int64)
+    n = csr.num_nodes
+    deg = (rp[1:] - rp[:-1])[order]
+    sptr = torch.zeros(n + 1, dtype=torch.int64, device=rp.device)
+    sptr[1:] = deg.cumsum(0)
+    e = csr.num_edges  # output sizes given: no device -> host sync (graph-capture safe)
+    offs = torch.arange(e, device=rp.device) - torch.repeat_interleave(sptr[:-1], deg,
+                                                                         output_size=e)
+    idx = torch.repeat_interleave(rp[order], deg, output_size=e) + offs
+    return SchedCSR(sptr[:-1].to(torch.int32).contiguous(), sptr[1:].to(torch.int32).contiguous(),
+                    csr.col[idx].contiguous())
+
+
+_sched_cache = {}
+
+
+def sched_csr(csr: "CSRGraph") -> Optional[SchedCSR]:
+    """The scheduled copy of ``csr`` for the eval forward (built on first use,
+    kept while ``csr.rowptr`` lives), or None: long rows (E'/N >=
+    SCHED_MAX_EPR: the prologue is a small share, and the copy would double a
+    large col array), split hub rows (they have their own schedule), no row
+    order, or GAT_EDGE_SCHED=0 (A/B knob).  Costs E' * 4 + N * 8 bytes."""
+    if (tuning.get("GAT_EDGE_SCHED") == "0" or csr.order is None or csr.hubs is not None
+            or csr.num_nodes == 0 or csr.num_edges // csr.num_nodes >= SCHED_MAX_EPR):
+        return None
+    key = id(csr.rowptr)
+    hit = _sched_cache.get(key)
+    if hit is not None and hit[0]() is csr.rowptr:
+        return hit[1]
+    sc = build_sched_csr(csr)
+    _sched_cache[key] = (weakref.ref(csr.rowptr), sc)
+    weakref.finalize(csr.rowptr, _sched_cache.pop, key, None)
+    return sc
+
+
 class _CSRCache:
     """Small LRU of CSRs keyed by the identity and version of ``edge_index``."""
 

@@ -27,7 +27,7 @@ from typing import NamedTuple, Optional, Tuple
 import torch
 
 from . import _lib, tuning
-from .graph import CSRGraph, get_csr
+from .graph import CSRGraph, get_csr, sched_csr
 
 __all__ = ["GraphAttentionLayer", "GraphAttentionLayerActivationTest", "score_activation_code",
            "PackedParams", "pack_params", "gat_forward", "ForwardPlan", "wh_slices", "NodeTable",
@@ -303,7 +303,7 @@ class ForwardPlan:
     two phases of exactly the path the layer runs."""
 
     __slots__ = ("n", "fin", "heads", "f", "hf", "hfp", "concat", "slope", "slices", "split",
-                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint")
+                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched")
 
     def __init__(self, x: torch.Tensor, csr: CSRGraph, heads: int, f: int, concat: bool,
                  negative_slope: float):
@@ -322,6 +322,11 @@ class ForwardPlan:
         # the kernels' hint: + GAT_HINT_LOCAL for a local graph (CSRGraph.kernel_hint)
         self.khint = csr.kernel_hint() if hasattr(csr, "kernel_hint") else self.hint
         self.split = csr.hubs is not None and fused_score_ok(heads, f, negative_slope)
+        # short rows: the edge kernel walks a scheduled copy of the CSR (graph.SchedCSR)
+        self.sched = None
+        if (not self.split and fused_score_ok(heads, f, negative_slope)
+                and isinstance(csr, CSRGraph)):
+            self.sched = sched_csr(csr)
 
     def project(self, lib, x: torch.Tensor, pp: PackedParams) -> None:
         """gat_project(_sliced) into the workspace (GAT.py:42-52)."""
@@ -356,6 +361,17 @@ class ForwardPlan:
                        self.concat, self.slope, bias, out, stream)
             return out
         p_order = 0 if csr.order is None else csr.order.data_ptr()
+        sc = self.sched
+        if sc is not None:
+            ld = self.hf // self.slices if self.slices > 1 else self.hfp
+            rc = lib.gat_edge_aggregate_seg(
+                sc.b.data_ptr(), sc.e.data_ptr(), 1, sc.col.data_ptr(), p_order, 0, n, self.p_wh,
+                ld, n, self.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
+                int(self.concat), self.slope, 0, 0, 0, 0, bias.data_ptr(), out.data_ptr(),
+                self.khint, stream)
+            if rc:
+                _lib.check(rc, "gat_edge_aggregate_seg (scheduled CSR)")
+            return out
         if self.slices > 1:
             rc = lib.gat_edge_aggregate_sliced(
                 csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, self.p_wh, n,
@@ -373,6 +389,9 @@ class ForwardPlan:
         return out
 
     def kernel_name(self) -> str:
+        if self.sched is not None:
+            return (f"gat_edge_aggregate_seg (k_edge_grp over the scheduled CSR"
+                    + (f", {self.slices} column planes)" if self.slices > 1 else ")"))
         if self.split:
             return "gat_edge_aggregate_seg (k_edge_grp, hub rows split) + gat_edge_merge"
         if self.slices > 1:

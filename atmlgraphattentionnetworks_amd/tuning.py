@@ -13,7 +13,7 @@ import os
 from typing import Dict, Optional
 
 # knobs read on the Python side of the boundary
-PY_KNOBS = ("GAT_WH_SLICES", "GAT_EDGE_ORDER", "GAT_HUB_SPLIT", "GAT_HUB_SEG")
+PY_KNOBS = ("GAT_WH_SLICES", "GAT_EDGE_ORDER", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_SCHED")
 
 _values: Dict[str, Optional[str]] = {}
 

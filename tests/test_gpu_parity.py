@@ -33,8 +33,10 @@ VARIANTS = {
     "u16": {"GAT_EDGE_U": "16"},
     "v2_natural": {"GAT_EDGE_V": "2", "GAT_EDGE_ORDER": "natural"},
     "pipe_u16_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
-    "gather_score": {"GAT_EDGE_SCORE": "gather"},
-    "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds"},
+    "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
+    "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds", "GAT_EDGE_SCHED": "0"},
+    # the CSR-order launch (short rows take the scheduled copy by default)
+    "nosched": {"GAT_EDGE_SCHED": "0"},
     # projection: k_project_x3 for 64 < fin <= 128 (WRES=0), k_project_wres for
     # every fin <= 128, the tiled fallback; plain stores instead of write-through
     "proj_wk": {"GAT_PROJ_WRES": "0"},
@@ -52,7 +54,7 @@ VARIANTS = {
 def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
-              "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT",
+              "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():

@@ -93,7 +93,7 @@ def main():
     bias = layer.bias.detach()
     specs = [s.strip() for s in args.variants.split(";") if s.strip()]
     envs = [parse(s) for s in specs]
-    knob_envs = [{k: v for k, v in e.items() if k not in ("passes", "sched", "hubseg")}
+    knob_envs = [{k: v for k, v in e.items() if k not in ("passes", "sched", "hubseg", "hublast")}
                  for e in envs]
 
     plan_out = {}
@@ -183,8 +183,50 @@ def main():
             return (f"hub segments of {self.seg_len} ({0 if h is None else h.n_hub} hubs, "
                     f"{0 if h is None else h.n_vrows} segments): " + self.plan.kernel_name())
 
+    class HubLast:
+        """Hub rows split as the default plan, but the whole rows run FIRST and
+        the hub segments after them (two launches of the same schedule's
+        position ranges), then the merge."""
+
+        def __init__(self, plan):
+            self.plan = plan
+
+        def edge(self, lib, csr_, pp_, bias_, out):
+            p = self.plan
+            hubs = csr.hubs
+            stream = torch._C._cuda_getCurrentRawStream(dev.index)
+            hf4 = (hf + 3) // 4 * 4
+            nv = hubs.n_vrows
+            st = torch.empty(nv * (hf4 + 2 * H), dtype=torch.float32, device=dev)
+            p_acc = st.data_ptr()
+            p_ml = p_acc + 4 * nv * hf4
+            n_pos = hubs.sched_row.numel()
+            ld = hf // p.slices if p.slices > 1 else p.hfp
+            for lo, hi in ((nv, n_pos), (0, nv)):
+                rc = lib.gat_edge_aggregate_seg(
+                    hubs.sched_b.data_ptr(), hubs.sched_e.data_ptr(), 1, csr.col.data_ptr(),
+                    hubs.sched_row.data_ptr(), lo, hi, p.p_wh, ld, n, p.slices,
+                    pp.a_src.data_ptr(), pp.c_src.data_ptr(), p.p_sd, H, F, int(w.concat), 0.2,
+                    p_acc, p_ml, 0, nv, bias.data_ptr(), out.data_ptr(), p.khint, stream)
+                _lib.check(rc, "hub-last seg")
+            rc = lib.gat_edge_merge(hubs.hub_rows.data_ptr(), hubs.hub_vptr.data_ptr(), hubs.n_hub,
+                                    p_acc, p_ml, H, F, int(w.concat), bias.data_ptr(),
+                                    out.data_ptr(), 0, 0, stream)
+            _lib.check(rc, "merge")
+            return out
+
+        def kernel_name(self):
+            return "hub segments last: " + self.plan.kernel_name()
+
     def plan_for(env):
         env = dict(env)
+        if int(env.pop("hublast", "0")):
+            apply(env)
+            plan = ForwardPlan(x, csr, w.heads, w.out_channels, w.concat, 0.2)
+            plan.project(lib, x, pp)
+            plan = HubLast(plan)
+            plan_out[id(plan)] = torch.empty(n, hf if w.concat else F, device=dev)
+            return plan
         windows = int(env.pop("passes", "0"))
         sched = int(env.pop("sched", "0"))
         hubseg = int(env.pop("hubseg", "0"))
