@@ -20,6 +20,7 @@ No PyG import, no CPU path: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import weakref
 from typing import NamedTuple, Optional, Tuple
@@ -303,7 +304,7 @@ class ForwardPlan:
     two phases of exactly the path the layer runs."""
 
     __slots__ = ("n", "fin", "heads", "f", "hf", "hfp", "concat", "slope", "slices", "split",
-                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched")
+                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched", "csr", "bound")
 
     def __init__(self, x: torch.Tensor, csr: CSRGraph, heads: int, f: int, concat: bool,
                  negative_slope: float):
@@ -327,6 +328,53 @@ class ForwardPlan:
         if (not self.split and fused_score_ok(heads, f, negative_slope)
                 and isinstance(csr, CSRGraph)):
             self.sched = sched_csr(csr)
+        self.csr = csr
+        self.bound = None  # (pp, bias, lib, project call, edge call) for run()
+
+    def run(self, lib, x: torch.Tensor, pp: PackedParams, bias: torch.Tensor,
+            out: torch.Tensor) -> torch.Tensor:
+        """project() + edge() for a plan the layer caches between forwards: the
+        argument lists (everything but x, out and the stream) are bound once
+        per (parameters, bias), so a forward costs two C-ABI calls and little
+        Python.  Safe to reuse the workspace: calls on one stream run in order,
+        and the layer keys its cached plans by stream."""
+        b = self.bound
+        if b is None or b[0] is not pp or b[1] != bias.data_ptr() or b[2] is not lib or \
+                self.split or self.slices == 1 and b[5]:
+            if self.split or self.sched is None:
+                self.project(lib, x, pp)
+                return self.edge(lib, self.csr, pp, bias, out)
+            b = self.bound = self._bind(lib, pp, bias)
+        stream = torch._C._cuda_getCurrentRawStream(self.dev)
+        rc = b[3](x.data_ptr(), *b[4], stream)
+        if rc:
+            if rc == _lib.GAT_EUNSUPPORTED and self.slices > 1:
+                self.bound = None  # fall back to the row-major table (project() decides)
+                self.project(lib, x, pp)
+                return self.edge(lib, self.csr, pp, bias, out)
+            _lib.check(rc, "gat_project")
+        rc = b[6](*b[7], out.data_ptr(), self.khint, stream)
+        if rc:
+            _lib.check(rc, "gat_edge_aggregate_seg (scheduled CSR)")
+        return out
+
+    def _bind(self, lib, pp: PackedParams, bias: torch.Tensor):
+        n, fin, heads, f, sc = self.n, self.fin, self.heads, self.f, self.sched
+        pw = (pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+              pp.a_dst.data_ptr(), pp.c_dst.data_ptr())
+        if self.slices > 1:
+            pfn = lib.gat_project_sliced
+            pargs = (n, fin, *pw, heads, f, self.slices, self.p_wh, n, 0, heads, self.p_sd)
+        else:
+            pfn = lib.gat_project
+            pargs = (n, fin, *pw, heads, f, self.p_wh, self.hfp, self.p_ss, heads, self.p_sd)
+        ld = self.hf // self.slices if self.slices > 1 else self.hfp
+        p_order = 0 if self.csr.order is None else self.csr.order.data_ptr()
+        eargs = (sc.b.data_ptr(), sc.e.data_ptr(), 1, sc.col.data_ptr(), p_order, 0, n, self.p_wh,
+                 ld, n, self.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
+                 int(self.concat), self.slope, 0, 0, 0, 0, bias.data_ptr())
+        return (pp, bias.data_ptr(), lib, pfn, pargs, self.slices > 1,
+                lib.gat_edge_aggregate_seg, eargs)
 
     def project(self, lib, x: torch.Tensor, pp: PackedParams) -> None:
         """gat_project(_sliced) into the workspace (GAT.py:42-52)."""
@@ -579,8 +627,29 @@ class GraphAttentionLayer(torch.nn.Module):
             from .training import gat_train_forward, next_seed_slot
             slot = next_seed_slot(self, x.device) if p > 0.0 else None
             return gat_train_forward(self, x, csr, p, 0, act, act_param, seed_slot=slot)
-        return gat_forward(x, csr, self.packed(), self.bias.detach(), self.num_heads,
-                           self.output_channels, self.concat, act_param)
+        return self._eval_forward(x, csr, act_param)
+
+    def _eval_forward(self, x: torch.Tensor, csr: CSRGraph, slope: float) -> torch.Tensor:
+        """The eval forward (GAT.py:37-67, no autograd, no dropout) through a
+        ForwardPlan cached per (graph, x shape, slope, stream): its workspace
+        and bound argument lists are reused, so a forward allocates only its
+        output.  Small graphs (the CIFAR batch: ~15 us of GPU work) are
+        host-bound, and this path is most of their host cost."""
+        plans = self.__dict__.get("_eval_plans")
+        if plans is None:
+            plans = self.__dict__["_eval_plans"] = collections.OrderedDict()
+        dev = x.device.index
+        key = (id(csr), x.shape[0], x.shape[1], slope, dev,
+               torch._C._cuda_getCurrentRawStream(dev), tuning.generation)
+        plan = plans.get(key)
+        if plan is None or plan.csr is not csr:
+            plan = plans[key] = ForwardPlan(x, csr, self.num_heads, self.output_channels,
+                                            self.concat, slope)
+            while len(plans) > 4:
+                plans.popitem(last=False)
+        out = torch.empty(plan.n, plan.hf if self.concat else self.output_channels,
+                          dtype=torch.float32, device=x.device)
+        return plan.run(_lib.load(), x, self.packed(), self.bias.detach(), out)
 
     def extra_repr(self) -> str:
         return (f"{self.input_channels}, {self.output_channels}, num_heads={self.num_heads}, "

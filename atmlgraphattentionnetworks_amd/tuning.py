@@ -16,12 +16,16 @@ from typing import Dict, Optional
 PY_KNOBS = ("GAT_WH_SLICES", "GAT_EDGE_ORDER", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_SCHED")
 
 _values: Dict[str, Optional[str]] = {}
+# bumped by every reload(): cached launch plans (layer.ForwardPlan) key on it,
+# so a knob change reaches the next forward
+generation = 0
 
 
 def reload() -> None:
     """Re-read the environment (Python knobs and the library's snapshot)."""
-    global _values
+    global _values, generation
     _values = {k: os.environ.get(k) for k in PY_KNOBS}
+    generation += 1
     from . import _lib
     if _lib.is_loaded():
         _lib.load().gat_tuning_reload()
