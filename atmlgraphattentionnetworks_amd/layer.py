@@ -301,22 +301,38 @@ class ForwardPlan:
     """The eval forward's launch plan for one (x, graph, layer shape): the
     workspace (Wh | s_src | s_dst), the table layout and the edge path.
     ``gat_forward`` builds one per call; ``bench.py`` keeps one to time the
-    two phases of exactly the path the layer runs."""
+    two phases of exactly the path the layer runs.
+
+    ``pingpong``: two workspaces, used by alternate ``run()`` calls.  A kernel
+    that writes lines the previous kernel gathered from pays for it on this
+    GPU (tools/proj_floor.hip: an 11.5-MB streaming write behind a kernel that
+    read those lines takes 12.0 us instead of 4.3; the PPI projection 13.8 us
+    instead of 10.0), so a layer applied back to back (the layer's cached plan)
+    projects into the table the previous forward did NOT read."""
 
     __slots__ = ("n", "fin", "heads", "f", "hf", "hfp", "concat", "slope", "slices", "split",
-                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched", "csr", "bound")
+                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched", "csr", "bound",
+                 "bufs", "cur")
 
     def __init__(self, x: torch.Tensor, csr: CSRGraph, heads: int, f: int, concat: bool,
-                 negative_slope: float):
+                 negative_slope: float, pingpong: bool = False):
         n, fin = x.shape
         self.n, self.fin, self.heads, self.f, self.concat = n, fin, heads, f, concat
         self.slope = float(negative_slope)
         self.hf = heads * f
         self.hfp = (self.hf + 3) // 4 * 4
-        self.ws = torch.empty(n * (self.hfp + 2 * heads), dtype=torch.float32, device=x.device)
-        self.p_wh = self.ws.data_ptr()
-        self.p_ss = self.p_wh + 4 * n * self.hfp
-        self.p_sd = self.p_ss + 4 * n * heads
+        per = n * (self.hfp + 2 * heads)
+        # each workspace starts on a 256-B boundary (the kernels' row alignment)
+        per_al = (per + 63) // 64 * 64
+        nbuf = 2 if pingpong else 1
+        self.ws = torch.empty(per_al * nbuf, dtype=torch.float32, device=x.device)
+        self.bufs = []
+        for i in range(nbuf):
+            p_wh = self.ws.data_ptr() + 4 * per_al * i
+            p_ss = p_wh + 4 * n * self.hfp
+            self.bufs.append((p_wh, p_ss, p_ss + 4 * n * heads))
+        self.cur = 0
+        self.p_wh, self.p_ss, self.p_sd = self.bufs[0]
         self.dev = x.device.index
         self.hint = csr.num_edges // max(n, 1)
         self.slices = wh_slices(heads, f, concat, negative_slope, self.hint)
@@ -338,6 +354,9 @@ class ForwardPlan:
         per (parameters, bias), so a forward costs two C-ABI calls and little
         Python.  Safe to reuse the workspace: calls on one stream run in order,
         and the layer keys its cached plans by stream."""
+        if len(self.bufs) > 1:  # alternate workspaces (pingpong)
+            self.cur ^= 1
+            self.p_wh, self.p_ss, self.p_sd = self.bufs[self.cur]
         b = self.bound
         if b is None or b[0] is not pp or b[1] != bias.data_ptr() or b[2] is not lib or \
                 self.split or self.slices == 1 and b[5]:
@@ -346,14 +365,14 @@ class ForwardPlan:
                 return self.edge(lib, self.csr, pp, bias, out)
             b = self.bound = self._bind(lib, pp, bias)
         stream = torch._C._cuda_getCurrentRawStream(self.dev)
-        rc = b[3](x.data_ptr(), *b[4], stream)
+        rc = b[3](x.data_ptr(), *b[4][self.cur], stream)
         if rc:
             if rc == _lib.GAT_EUNSUPPORTED and self.slices > 1:
                 self.bound = None  # fall back to the row-major table (project() decides)
                 self.project(lib, x, pp)
                 return self.edge(lib, self.csr, pp, bias, out)
             _lib.check(rc, "gat_project")
-        rc = b[6](*b[7], out.data_ptr(), self.khint, stream)
+        rc = b[6](*b[7][self.cur], out.data_ptr(), self.khint, stream)
         if rc:
             _lib.check(rc, "gat_edge_aggregate_seg (scheduled CSR)")
         return out
@@ -362,17 +381,20 @@ class ForwardPlan:
         n, fin, heads, f, sc = self.n, self.fin, self.heads, self.f, self.sched
         pw = (pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(), pp.c_src.data_ptr(),
               pp.a_dst.data_ptr(), pp.c_dst.data_ptr())
-        if self.slices > 1:
-            pfn = lib.gat_project_sliced
-            pargs = (n, fin, *pw, heads, f, self.slices, self.p_wh, n, 0, heads, self.p_sd)
-        else:
-            pfn = lib.gat_project
-            pargs = (n, fin, *pw, heads, f, self.p_wh, self.hfp, self.p_ss, heads, self.p_sd)
         ld = self.hf // self.slices if self.slices > 1 else self.hfp
         p_order = 0 if self.csr.order is None else self.csr.order.data_ptr()
-        eargs = (sc.b.data_ptr(), sc.e.data_ptr(), 1, sc.col.data_ptr(), p_order, 0, n, self.p_wh,
-                 ld, n, self.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
-                 int(self.concat), self.slope, 0, 0, 0, 0, bias.data_ptr())
+        pargs, eargs = [], []
+        for p_wh, p_ss, p_sd in self.bufs:  # one argument list per workspace
+            if self.slices > 1:
+                pfn = lib.gat_project_sliced
+                pargs.append((n, fin, *pw, heads, f, self.slices, p_wh, n, 0, heads, p_sd))
+            else:
+                pfn = lib.gat_project
+                pargs.append((n, fin, *pw, heads, f, p_wh, self.hfp, p_ss, heads, p_sd))
+            eargs.append((sc.b.data_ptr(), sc.e.data_ptr(), 1, sc.col.data_ptr(), p_order, 0, n,
+                          p_wh, ld, n, self.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+                          p_sd, heads, f, int(self.concat), self.slope, 0, 0, 0, 0,
+                          bias.data_ptr()))
         return (pp, bias.data_ptr(), lib, pfn, pargs, self.slices > 1,
                 lib.gat_edge_aggregate_seg, eargs)
 
@@ -644,7 +666,7 @@ class GraphAttentionLayer(torch.nn.Module):
         plan = plans.get(key)
         if plan is None or plan.csr is not csr:
             plan = plans[key] = ForwardPlan(x, csr, self.num_heads, self.output_channels,
-                                            self.concat, slope)
+                                            self.concat, slope, pingpong=True)
             while len(plans) > 4:
                 plans.popitem(last=False)
         out = torch.empty(plan.n, plan.hf if self.concat else self.output_channels,
