@@ -1066,7 +1066,14 @@ __host__ __device__ inline int wk_lds_floats(int fin, int nt) {
     return wk_param_offset(fin, nt) + 3 * nt * 16 + 128;
 }
 
-template <int NT>
+// DIRECT (F in {4, 8, 16}): the MFMA operands are swapped (A = W fragment,
+// B = x fragment), so the accumulator holds C^T: lane l has Wh[row l&15]
+// [16t + 4(l>>4) .. +4], four consecutive columns of one row.  The epilogue
+// then stores float4s straight from the accumulators and forms each head's
+// scores by a DPP/xor sum over the F/4 lanes of the head: no output tile in
+// LDS, no third barrier, no index divisions (PPI: tools/proj_floor.hip
+// measured the projection's VALU count as what bounds it after the loads).
+template <int NT, bool DIRECT = false>
 __global__ __launch_bounds__(256) void k_project_wk(
     const float* __restrict__ X, int n, int fin,
     const float* __restrict__ W, const float* __restrict__ bW,
@@ -1157,13 +1164,18 @@ __global__ __launch_bounds__(256) void k_project_wk(
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int t = 0; t < NT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bq[u][t], acc[t], 0, 0, 0);
+                acc[t] = DIRECT
+                    ? __builtin_amdgcn_mfma_f32_16x16x4f32(bq[u][t], a[u], acc[t], 0, 0, 0)
+                    : __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bq[u][t], acc[t], 0, 0, 0);
     }
     for (; s < ks; ++s) {
         const float a = xa[4 * s];
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[t * 16 * fin + 4 * s], acc[t], 0, 0, 0);
+        for (int t = 0; t < NT; ++t) {
+            const float b = wb[t * 16 * fin + 4 * s];
+            acc[t] = DIRECT ? __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, acc[t], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+        }
     }
     if (fin & 3) {  // last partial k-step
         const bool ok = 4 * ks + kq < fin;
@@ -1171,8 +1183,43 @@ __global__ __launch_bounds__(256) void k_project_wk(
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const float b = ok ? wb[t * 16 * fin + 4 * ks] : 0.f;
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+            acc[t] = DIRECT ? __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, acc[t], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
         }
+    }
+    if constexpr (DIRECT) {
+        // lane: row w*16 + cl, columns c0 = 16t + 4kq .. +4 of every tile t
+        const int row = row0 + w * 16 + cl;
+        const int hfp = round_up4(HF);
+        const int hl = F >> 2;  // lanes (kq) per head: 1, 2 or 4
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int c0 = 16 * t + 4 * kq;
+            const f32x4 v = acc[t] + *reinterpret_cast<const f32x4*>(bs + c0);
+            const f32x4 q1 = *reinterpret_cast<const f32x4*>(a1s + c0);
+            const f32x4 q2 = *reinterpret_cast<const f32x4*>(a2s + c0);
+            float p1 = v.x * q1.x + v.y * q1.y + v.z * q1.z + v.w * q1.w;
+            float p2 = v.x * q2.x + v.y * q2.y + v.z * q2.z + v.w * q2.w;
+            if (hl >= 2) {
+                p1 += __shfl_xor(p1, 16);
+                p2 += __shfl_xor(p2, 16);
+            }
+            if (hl >= 4) {
+                p1 += __shfl_xor(p1, 32);
+                p2 += __shfl_xor(p2, 32);
+            }
+            if (row < n && c0 < hfp) {
+                const int g = c0 / slice_w;  // slice_w % 4 == 0: one plane per float4
+                store_out4(Wh, (size_t)g * (size_t)slice_stride + (size_t)row * ld_wh +
+                                   (c0 - g * slice_w), v, store_wt);
+                if ((kq & (hl - 1)) == 0 && c0 < HF) {
+                    const int h = c0 / F;
+                    if (Ss != nullptr) store_out1(Ss, (size_t)row * ld_s + h, p1 + c1s[h], store_wt);
+                    store_out1(s_dst, (size_t)row * H + h, p2 + c2s[h], store_wt);
+                }
+            }
+        }
+        return;
     }
     __syncthreads();  // X/W tiles dead: reuse LDS for the output tile
 
@@ -2753,7 +2800,7 @@ const char* const kKnobNames[] = {
     "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
     "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
     "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS", "GAT_BWD_KINK",
-    "GAT_WGRAD_LW",    "GAT_STORE_WT"};
+    "GAT_WGRAD_LW",    "GAT_STORE_WT",    "GAT_PROJ_WK_DIRECT"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -2894,11 +2941,20 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     const bool wk_ok = fin > 0 && fin <= wk_max && aligned16 && wk_lds <= 160 * 1024 &&
                        (pk == nullptr || std::strcmp(pk, "wk") == 0);
     if (wk_ok) {
+        // the direct epilogue for heads of 4, 8 or 16 columns (GAT_PROJ_WK_DIRECT=0:
+        // the LDS output tile, A/B knob)
+        bool direct = f == 4 || f == 8 || f == 16;
+        if (const char* v = knob("GAT_PROJ_WK_DIRECT")) direct = direct && std::atoi(v) != 0;
 #define GAT_WK_CASE(NT)                                                                       \
     case NT:                                                                                  \
-        hipLaunchKernelGGL((k_project_wk<NT>), grid, block, wk_lds, st, x, n, fin, w, b,      \
-                           a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s,  \
-                           s_dst, slice_w, slice_stride, store_wt);                           \
+        if (direct)                                                                           \
+            hipLaunchKernelGGL((k_project_wk<NT, true>), grid, block, wk_lds, st, x, n, fin,  \
+                               w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh,     \
+                               s_src, ld_s, s_dst, slice_w, slice_stride, store_wt);          \
+        else                                                                                  \
+            hipLaunchKernelGGL((k_project_wk<NT>), grid, block, wk_lds, st, x, n, fin, w, b,  \
+                               a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src,    \
+                               ld_s, s_dst, slice_w, slice_stride, store_wt);                 \
         break;
         switch (nt) {
             GAT_WK_CASE(1) GAT_WK_CASE(2) GAT_WK_CASE(3) GAT_WK_CASE(4)

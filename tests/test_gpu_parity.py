@@ -42,6 +42,7 @@ VARIANTS = {
     "proj_wk": {"GAT_PROJ_WRES": "0"},
     "proj_wres": {"GAT_PROJ_WRES": "1"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
+    "proj_wk_lds_epilogue": {"GAT_PROJ_WK_DIRECT": "0"},
     "plain_stores": {"GAT_STORE_WT": "0"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
@@ -55,7 +56,7 @@ def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
-              "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS"):
+              "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)

@@ -122,7 +122,12 @@ __device__ __forceinline__ void split3_8(const float* f, bf16x8& h1, bf16x8& h2,
 // fragments and keeps them split in registers.  x: each wave's 16-row tile is
 // contiguous in HBM, loaded coalesced (float4) one tile ahead into registers,
 // written to a wave-private LDS tile, fragments read back from there.
-template <int NT, int KS, int LR>
+// MODE (ablation): bit 0 no s_dst stores, bit 1 no Wh stores, bit 2 plain
+// (not write-through) stores, bit 3 no MFMA (x sums stand in), bit 4 the
+// output tile and scores go through a wave-private LDS tile so that Wh and
+// s_dst leave as whole coalesced rows (a 16-row tile of one plane is
+// contiguous in HBM)
+template <int NT, int KS, int LR, int MODE = 0>
 __global__ __launch_bounds__(256, 2) void k_proj_rt(
     const float* __restrict__ X, int n, int fin, const float* __restrict__ W,
     const float* __restrict__ bW, const float* __restrict__ a1, const float* __restrict__ c1,
@@ -135,6 +140,8 @@ __global__ __launch_bounds__(256, 2) void k_proj_rt(
     using rvec = typename std::conditional<LR == 2, f32x2, float>::type;
     __shared__ __attribute__((aligned(16))) float xs_all[4][XS];
     __shared__ __attribute__((aligned(16))) float ws[16 * NT * KP + KP];
+    constexpr int OS = 16 * NT + 4;
+    __shared__ __attribute__((aligned(16))) float os_all[4][16 * OS + 16 * 16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int cl = lane & 15, kq = lane >> 4;
     const int tiles = (n + 15) / 16;
@@ -213,6 +220,12 @@ __global__ __launch_bounds__(256, 2) void k_proj_rt(
         f32x4 acc[NT], cor[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t] = cor[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr ((MODE & 8) != 0) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int k = 0; k < KL; ++k) acc[t][k & 3] += f[k];
+        } else
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2)
 #pragma unroll
@@ -226,6 +239,40 @@ __global__ __launch_bounds__(256, 2) void k_proj_rt(
             }
         const int row = tile * 16 + cl;
         const bool rok = row < n;
+        if constexpr ((MODE & 16) != 0) {
+            float* os = os_all[w];
+            float* sc = os + 16 * OS;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const f32x4 v = acc[t] + cor[t] + bb[t];
+                const int c0 = 16 * t + 4 * kq;
+                float p2 = v.x * p2v[t].x + v.y * p2v[t].y + v.z * p2v[t].z + v.w * p2v[t].w;
+                for (int o = 16; o < 16 * hl; o <<= 1) p2 += __shfl_xor(p2, o);
+                *reinterpret_cast<f32x4*>(os + cl * OS + c0) = v;
+                if (c0 < HF && (kq & (hl - 1)) == 0) sc[cl * H + c0 / F] = p2 + cs2[t];
+            }
+            __builtin_amdgcn_wave_barrier();
+            const int row0 = tile * 16;
+            const int sw4 = slice_w >> 2, lsw = 31 - __builtin_clz((unsigned)sw4);
+            const int planes = (HF + slice_w - 1) / slice_w;
+            for (int g = 0; g < planes; ++g)
+                for (int q = lane; q < 16 * sw4; q += 64) {
+                    const int r = q >> lsw, c4 = q & (sw4 - 1);
+                    if (row0 + r < n)
+                        st_wt4(Wh, (size_t)g * slice_stride + (size_t)(row0 + r) * slice_w + 4 * c4,
+                               *reinterpret_cast<const f32x4*>(os + r * OS + g * slice_w + 4 * c4));
+                }
+            // s_dst rows of the tile: 16 * H contiguous floats (H % 4 == 0 here)
+            const int h4 = H >> 2;
+            for (int q = lane; q < 16 * h4; q += 64) {
+                const int r = q / h4, c4 = q - r * h4;
+                if (row0 + r < n)
+                    st_wt4(s_dst, (size_t)(row0 + r) * H + 4 * c4,
+                           *reinterpret_cast<const f32x4*>(sc + r * H + 4 * c4));
+            }
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const f32x4 v = acc[t] + cor[t] + bb[t];
@@ -234,9 +281,131 @@ __global__ __launch_bounds__(256, 2) void k_proj_rt(
             for (int o = 16; o < 16 * hl; o <<= 1) p2 += __shfl_xor(p2, o);
             if (rok && c0 < HF) {
                 const int g = c0 / slice_w;
-                st_wt4(Wh, (size_t)g * slice_stride + (size_t)row * slice_w + (c0 - g * slice_w), v);
-                if ((kq & (hl - 1)) == 0) st_wt1(s_dst, (size_t)row * H + c0 / F, p2 + cs2[t]);
+                const size_t o = (size_t)g * slice_stride + (size_t)row * slice_w + (c0 - g * slice_w);
+                if constexpr ((MODE & 2) == 0) {
+                    if constexpr ((MODE & 4) != 0) *reinterpret_cast<f32x4*>(Wh + o) = v;
+                    else st_wt4(Wh, o, v);
+                }
+                if constexpr ((MODE & 1) == 0) {
+                    if ((kq & (hl - 1)) == 0) {
+                        if constexpr ((MODE & 4) != 0) s_dst[(size_t)row * H + c0 / F] = p2 + cs2[t];
+                        else st_wt1(s_dst, (size_t)row * H + c0 / F, p2 + cs2[t]);
+                    }
+                }
             }
+        }
+    }
+}
+
+// One-shot workgroup of 64 rows (4 waves x 16-row tiles), as the library's
+// k_project_wk, but on the split-bf16 matrix cores: the x tile (fp32) and W
+// go to LDS with coalesced float4 loads; W is split ONCE per workgroup into
+// three bf16 planes [col][KP + 8]; each wave reads its x fragments (fp32,
+// zeroed past fin, split in registers) and the W planes' fragments, 6 MFMA
+// per (16-col tile, 32-deep k step).  Output straight from the accumulators
+// (lane: row l&15, 4 consecutive columns).
+template <int NT, int KS>
+__global__ __launch_bounds__(256) void k_proj_wk3(
+    const float* __restrict__ X, int n, int fin, const float* __restrict__ W,
+    const float* __restrict__ bW, const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int slice_w, long slice_stride,
+    float* __restrict__ s_dst) {
+    constexpr int KP = 32 * KS, WSB = KP + 8, BN = 16 * NT;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    __bf16* wsb = reinterpret_cast<__bf16*>(smem);            // [3][BN][WSB]
+    float* xs = smem + (3 * BN * WSB) / 2;                       // [64][fin] (+KP overhang)
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int row0 = blockIdx.x * 64;
+    const int rows = min(64, n - row0);
+    // x rows [row0, row0 + rows): one contiguous run; W [HF, fin] another
+    {
+        const int xc = rows * fin, xc4 = xc >> 2;
+        const float* xg = X + (size_t)row0 * fin;  // 64*fin*4*b bytes: 16-B aligned
+        constexpr int XIT = 64 * KP / 4 / 256;     // fin <= KP
+        f32x4 xv[XIT];
+#pragma unroll
+        for (int it = 0; it < XIT; ++it)
+            xv[it] = reinterpret_cast<const f32x4*>(xg)[min(tid + 256 * it, max(xc4 - 1, 0))];
+        // W: each thread splits 4 consecutive k of one column per step
+        constexpr int WIT = BN * KP / 4 / 256;
+        f32x4 wv[WIT];
+#pragma unroll
+        for (int it = 0; it < WIT; ++it) {
+            const int e = 4 * (tid + 256 * it), c = e / KP, k = e % KP;
+            const float* src = W + (size_t)min(c, HF - 1) * fin;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wv[it][j] = src[min(k + j, fin - 1)];
+        }
+#pragma unroll
+        for (int it = 0; it < XIT; ++it)
+            if (tid + 256 * it < xc4) reinterpret_cast<f32x4*>(xs)[tid + 256 * it] = xv[it];
+        for (int i = 4 * xc4 + tid; i < xc; i += 256) xs[i] = xg[i];
+#pragma unroll
+        for (int it = 0; it < WIT; ++it) {
+            const int e = 4 * (tid + 256 * it), c = e / KP, k = e % KP;
+            f32x4 v = wv[it];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (c < HF && k + j < fin) ? v[j] : 0.f;
+            bf16x2 p1a, p2a, p3a, p1b, p2b, p3b;
+            split3_pair(f32x2{v.x, v.y}, p1a, p2a, p3a);
+            split3_pair(f32x2{v.z, v.w}, p1b, p2b, p3b);
+            const int o = c * WSB + k;
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<bf16x4*>(wsb + o) = bf16x4{p1a[0], p1a[1], p1b[0], p1b[1]};
+            *reinterpret_cast<bf16x4*>(wsb + BN * WSB + o) = bf16x4{p2a[0], p2a[1], p2b[0], p2b[1]};
+            *reinterpret_cast<bf16x4*>(wsb + 2 * BN * WSB + o) = bf16x4{p3a[0], p3a[1], p3b[0], p3b[1]};
+        }
+    }
+    __syncthreads();
+    const int r = w * 16 + cl;
+    bf16x8 x1[KS], x2[KS], x3[KS];
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+        float f[8];
+        const int k0 = 32 * s2 + 8 * kq;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = k0 + j < fin ? xs[r * fin + k0 + j] : 0.f;
+        split3_8(f, x1[s2], x2[s2], x3[s2]);
+    }
+    f32x4 acc[NT], cor[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = cor[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int o = (16 * t + cl) * WSB + 32 * s2 + 8 * kq;
+            const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(wsb + o);
+            const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(wsb + BN * WSB + o);
+            const bf16x8 b3 = *reinterpret_cast<const bf16x8*>(wsb + 2 * BN * WSB + o);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x1[s2], acc[t], 0, 0, 0);
+            cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, x1[s2], cor[t], 0, 0, 0);
+            cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x2[s2], cor[t], 0, 0, 0);
+            cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b3, x1[s2], cor[t], 0, 0, 0);
+            cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, x2[s2], cor[t], 0, 0, 0);
+            cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x3[s2], cor[t], 0, 0, 0);
+        }
+    const int row = row0 + r;
+    const int hl = F / 4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int c0 = 16 * t + 4 * kq;
+        f32x4 bb, p2v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool ok = c0 + i < HF;
+            bb[i] = ok ? bW[min(c0 + i, HF - 1)] : 0.f;
+            p2v[i] = ok ? a2[min(c0 + i, HF - 1)] : 0.f;
+        }
+        const f32x4 v = acc[t] + cor[t] + bb;
+        float p2 = v.x * p2v.x + v.y * p2v.y + v.z * p2v.z + v.w * p2v.w;
+        for (int o = 16; o < 16 * hl; o <<= 1) p2 += __shfl_xor(p2, o);
+        if (row < n && c0 < HF) {
+            const int g = c0 / slice_w;
+            st_wt4(Wh, (size_t)g * slice_stride + (size_t)row * slice_w + (c0 - g * slice_w), v);
+            if ((kq & (hl - 1)) == 0)
+                st_wt1(s_dst, (size_t)row * H + c0 / F, p2 + c2[min(c0 / F, H - 1)]);
         }
     }
 }
@@ -330,7 +499,7 @@ int main(int argc, char** argv) {
     };
     // parity of the prototype against the library
     lib();
-    rt((tiles + 3) / 4)();
+    k_proj_wk3<4, 2><<<(n + 63) / 64, 256, (3 * 64 * 72) * 2 + (64 * 64 + 64) * 4, st>>>(x, n, fin, w, b, a2, c2, H, F, HF, wh2, sw, (long)n * sw, sd2);
     CK(hipStreamSynchronize(st));
     {
         std::vector<float> A(nwh), B(nwh), SA((size_t)n * H), SB((size_t)n * H);
@@ -358,11 +527,25 @@ int main(int argc, char** argv) {
                          {"lib_project", lib}, {"lib_project_other_table", lib_to(wh2)}};
     const int rt_grids[] = {256, 512, 768, (tiles + 3) / 4};
     for (int wgs : rt_grids) vs.push_back({nullptr, rt(wgs)});
+#define RT_MODE(M, NM)                                                                          \
+    vs.push_back({NM, [&] {                                                                     \
+        k_proj_rt<4, 2, 2, M><<<512, 256, 0, st>>>(x, n, fin, w, b, a1, c1, a2, c2, H, F, HF,   \
+                                                   wh2, sw, (long)n * sw, sd2);                \
+    }});
+    RT_MODE(1, "rt512_no_sdst") RT_MODE(2, "rt512_no_wh") RT_MODE(3, "rt512_no_stores")
+    RT_MODE(4, "rt512_plain_stores") RT_MODE(8, "rt512_no_mfma") RT_MODE(11, "rt512_loads_only")
+    RT_MODE(16, "rt512_lds_epilogue")
+    const size_t wk3_lds = (3 * 64 * 72) * 2 + (64 * 64 + 64) * 4;
+    vs.push_back({"wk3", [&] { k_proj_wk3<4, 2><<<(n + 63) / 64, 256, wk3_lds, st>>>(x, n, fin, w, b, a2, c2, H, F, HF, wh2, sw, (long)n * sw, sd2); }});
+    vs.push_back({"rt256_lds_epilogue", [&] { k_proj_rt<4, 2, 2, 16><<<256, 256, 0, st>>>(x, n, fin, w, b, a1, c1, a2, c2, H, F, HF, wh2, sw, (long)n * sw, sd2); }});
+    vs.push_back({"rt768_lds_epilogue", [&] { k_proj_rt<4, 2, 2, 16><<<768, 256, 0, st>>>(x, n, fin, w, b, a1, c1, a2, c2, H, F, HF, wh2, sw, (long)n * sw, sd2); }});
+    vs.push_back({"rt384_lds_epilogue", [&] { k_proj_rt<4, 2, 2, 16><<<384, 256, 0, st>>>(x, n, fin, w, b, a1, c1, a2, c2, H, F, HF, wh2, sw, (long)n * sw, sd2); }});
+#undef RT_MODE
     for (size_t i = 0; i < vs.size(); ++i) {
         char nm[64];
         const char* name = vs[i].name;
         if (!name) {
-            snprintf(nm, sizeof nm, "rt_wg%d", rt_grids[i - (vs.size() - 4)]);
+            snprintf(nm, sizeof nm, "rt_wg%d", rt_grids[i - 7]);
             name = nm;
         }
         auto f = vs[i].f;
