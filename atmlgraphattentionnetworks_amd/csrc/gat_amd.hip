@@ -2705,6 +2705,67 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dwh, in
 // groups per block, 4 independent loads in flight per thread, then a fixed
 // order combine in LDS (deterministic).  Sums the per-chunk / per-wave
 // partials of k_wgrad and k_src_bwd.
+// ---------------------------------------------------------------------------
+// Input gradient of the projection: dx[n, fin] = dWh[n, hf] W[hf, fin] (the x
+// side of GAT.py:42-48's Linear layers; replaces the hipBLASLt GEMM).  fp32
+// MFMA (v_mfma_f32_16x16x4_f32, exact fp32 products) with the operands swapped
+// so the accumulator holds dx^T tiles: lane l ends with dx[row l&15][c + 4(l>>4)
+// .. +4], four consecutive columns of one row.  The K = hf sum runs as KL
+// k-steps per lane (lane kq owns k in [KL kq, KL kq + KL): every lane's dWh
+// fragment is one contiguous run of its row, loaded once); W^T is staged per
+// 64-column block in LDS (row stride KP + 1: conflict-free fragment reads).
+// A workgroup owns 64 rows (one 16-row tile per wave) and walks all fin
+// columns, so dWh is read once and W (hf x fin, L2-resident) once per
+// workgroup.
+// ---------------------------------------------------------------------------
+template <int KL>
+__global__ __launch_bounds__(256) void k_dx(const float* __restrict__ dwh, int ld_dwh, int hf,
+                                            int n, const float* __restrict__ W, int fin,
+                                            float* __restrict__ dx, int ld_dx) {
+    constexpr int KP = 4 * KL, WS = KP + 1;
+    __shared__ float wt[64 * WS];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int row = blockIdx.x * 64 + w * 16 + cl;
+    const int kb = KL * kq;
+    float b[KL];
+    {
+        const float* src = dwh + (size_t)min(row, n - 1) * ld_dwh;
+#pragma unroll
+        for (int s = 0; s < KL; ++s) b[s] = kb + s < hf ? src[min(kb + s, hf - 1)] : 0.f;
+    }
+    const bool pair = (ld_dx % 2) == 0 && (reinterpret_cast<uintptr_t>(dx) & 7) == 0;
+    for (int c0 = 0; c0 < fin; c0 += 64) {
+        __syncthreads();  // the previous block's fragment reads are done
+        for (int i = tid; i < 64 * KP; i += 256) {
+            const int c = i & 63, k = i >> 6;  // a wave reads 64 consecutive columns of W row k
+            wt[c * WS + k] = (k < hf && c0 + c < fin) ? W[(size_t)k * fin + c0 + c] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (c0 + 16 * t >= fin) break;  // block-uniform
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            const float* a = wt + (16 * t + cl) * WS + kb;
+#pragma unroll
+            for (int s = 0; s < KL; ++s)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
+            const int col = c0 + 16 * t + 4 * kq;
+            if (row < n) {
+                float* d = dx + (size_t)row * ld_dx + col;
+                if (col + 3 < fin && pair) {
+                    *reinterpret_cast<f32x2*>(d) = f32x2{acc.x, acc.y};
+                    *reinterpret_cast<f32x2*>(d + 2) = f32x2{acc.z, acc.w};
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (col + r < fin) d[r] = acc[r];
+                }
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ part, int rows,
                                                 long long width, float* __restrict__ out,
                                                 int rows_per_block) {
@@ -3807,6 +3868,29 @@ int gat_weight_grad(const float* x, int num_nodes, int fin, const float* dwh, in
     const long long count = (long long)hf * fin;
     hipLaunchKernelGGL(k_colsum, dim3((unsigned)((count + 15) / 16)), dim3(256), 0, st, part,
                        chunks, count, dw, chunks);
+    return status_of(hipGetLastError());
+}
+
+int gat_input_grad(const float* dwh, int ld_dwh, int num_nodes, int hf, const float* w,
+                   int fin, float* dx, int ld_dx, void* stream) {
+    if (num_nodes < 0 || fin <= 0 || hf <= 0 || ld_dwh < hf || ld_dx < fin) return GAT_EINVAL;
+    if (hf > 128) return GAT_EUNSUPPORTED;
+    if (num_nodes == 0) return GAT_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((num_nodes + 63) / 64), block(256);
+    // K = hf padded with zeros to 4 KL
+    const int kl = hf <= 8 ? 2 : hf <= 16 ? 4 : hf <= 32 ? 8 : hf <= 64 ? 16 : 32;
+#define GAT_DX(KLV)                                                                            \
+    hipLaunchKernelGGL(k_dx<KLV>, grid, block, 0, st, dwh, ld_dwh, hf, num_nodes, w, fin, dx, \
+                       ld_dx)
+    switch (kl) {
+        case 2: GAT_DX(2); break;
+        case 4: GAT_DX(4); break;
+        case 8: GAT_DX(8); break;
+        case 16: GAT_DX(16); break;
+        default: GAT_DX(32); break;
+    }
+#undef GAT_DX
     return status_of(hipGetLastError());
 }
 

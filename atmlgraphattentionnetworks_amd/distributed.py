@@ -265,10 +265,12 @@ class ShardedGAT:
 
     def __init__(self, layer, csr, world: int, rank: int, exchange: str = "allgather",
                  group=None, ops=None, packed=None, chunks: Optional[int] = None,
-                 exchanger=None, force_exchange: bool = False):
+                 exchanger=None, force_exchange: bool = False, pingpong: bool = True):
         """force_exchange: issue the chunk collectives even at world 1 (an
         in-place all-gather of a rank's own block), so the RCCL path can be
-        exercised on a one-GPU box (tests, ``bench.py --dist``)."""
+        exercised on a one-GPU box (tests, ``bench.py --dist``).
+        pingpong: ``forward()`` alternates two node tables (the phase_* methods
+        work on the current one)."""
         if exchange not in ("allgather", "replicate"):
             raise ValueError(exchange)
         self.layer, self.world, self.rank = layer, world, rank
@@ -323,7 +325,14 @@ class ShardedGAT:
         self.slices = slices
         self.wh_only = kind != "packed"
         self.local = self._local_csr(csr, e0, e1, dev)
-        self.table = torch.zeros(lay.numel, dtype=torch.float32, device=dev)
+        # two tables, used by alternate forward() calls: the projection and the
+        # all-gather then write lines the previous step's edge passes did not
+        # read (layer.ForwardPlan pingpong: writing lines another kernel just
+        # gathered from costs 12 vs 4.3 us per 11.5 MB on this GPU)
+        self.tables = [torch.zeros(lay.numel, dtype=torch.float32, device=dev)
+                       for _ in range(2 if pingpong else 1)]
+        self._tix = 0
+        self.table = self.tables[0]
         n_sd = csr.num_nodes if exchange == "replicate" else self.n_local
         self.s_dst = torch.empty(max(n_sd, 1), heads, dtype=torch.float32, device=dev)
         blk = lay.block_rows if exchange == "allgather" else csr.num_nodes
@@ -416,6 +425,9 @@ class ShardedGAT:
 
     def forward(self, xl):
         """One step: x = this rank's rows (allgather) or all rows (replicate)."""
+        if len(self.tables) > 1:
+            self._tix ^= 1
+            self.table = self.tables[self._tix]
         if self.exchange == "replicate":
             self.project_chunk(xl, 0)
             return self.edge_pass(0)
@@ -459,7 +471,7 @@ def _emulated_ranks(layer, csr, x, world: int, exchange: str, chunks: Optional[i
     """Every rank's ShardedGAT in one process, projected, tables filled by
     block copies (the all-gather's result)."""
     ranks = [ShardedGAT(layer, csr, world, r, exchange=exchange, chunks=chunks,
-                        exchanger=NoExchange()) for r in range(world)]
+                        exchanger=NoExchange(), pingpong=False) for r in range(world)]
     lay = ranks[0].layout
     for sh in ranks[1:]:
         # the layout fixes the collectives' sizes: every rank must agree

@@ -21,8 +21,8 @@ PyG's gather/scatter ops (``run_inductive.py:83-90``, ``run_*_experiment.py``:
             (other score activations or head widths: gat_edge_backward_rows,
             which stores (A, dz) per edge in CSC order, + gat_src_backward)
             3. gat_weight_grad: dW = dWh^T x (split-K fp32 MFMA)
-            4. dx = dWh W (hipBLASLt via torch.mm, a plain library GEMM), only
-               when x needs a gradient.
+            4. gat_input_grad: dx = dWh W (fp32 matrix cores), only when x
+               needs a gradient.
 
 The per-head parameters are views into the packed buffers the kernels read
 (``GraphAttentionLayer._bind_packed``), so the gradients come back as views of
@@ -148,7 +148,15 @@ class GATFunction(torch.autograd.Function):
         if dwh is None:
             dwh, ps = _backward_stored(ctx, g, ws, csc, stream)
         need = ctx.needs_input_grad
-        dx = torch.mm(dwh, pp.w) if need[0] else None
+        dx = None
+        if need[0]:  # dx = dWh W (gat_input_grad: fp32 matrix cores, hf <= 128)
+            dx = torch.empty(n, fin, dtype=torch.float32, device=dev)
+            rc = _lib.load().gat_input_grad(dwh.data_ptr(), dwh.stride(0), n, hf,
+                                            pp.w.data_ptr(), fin, dx.data_ptr(), fin, stream)
+            if rc == _lib.GAT_EUNSUPPORTED:
+                dx = torch.mm(dwh, pp.w)  # wider tables than any reference configuration
+            elif rc:
+                _lib.check(rc, "gat_input_grad")
         dbias = ps[3 * hf + 2 * heads:] if need[1] else None
         grads = [None] * (6 * heads)
         if any(need[5:]):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 5
+#define GAT_ABI_VERSION 6
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -424,6 +424,19 @@ int gat_weight_grad_workspace_size(int num_nodes, int fin, int hf, size_t* bytes
  */
 int gat_weight_grad(const float* x, int num_nodes, int fin, const float* dwh, int ld_dwh, int hf,
                     float* dw, void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Input gradient of gat_project: dx[num_nodes, fin] = dwh[num_nodes, hf] w[hf, fin]
+ * (the x side of cat_h ws[h], GAT.py:42-48; replaces the reference autograd's
+ * mm through each head's Linear).  fp32 matrix cores, exact fp32 products;
+ * every row's sum runs in one fixed order (deterministic).  hf <= 128
+ * (GAT_EUNSUPPORTED beyond).
+ *   dwh  [num_nodes, ld_dwh] (gat_bwd_sources' / gat_src_backward's dwh)
+ *   w    the packed projection weight [hf, fin] (gat_project's w)
+ *   dx   [num_nodes, ld_dx], ld_dx >= fin
+ */
+int gat_input_grad(const float* dwh, int ld_dwh, int num_nodes, int hf, const float* w,
+                   int fin, float* dx, int ld_dx, void* stream);
 
 /* Workspace bytes gat_sum_partials needs (0 for num_parts <= 256). */
 int gat_sum_partials_workspace_size(int num_parts, long long width, size_t* bytes);

@@ -488,3 +488,23 @@ def test_backward_on_a_100k_edge_hub_row(kink, monkeypatch):
     gout = torch.randn(n, H * F, generator=g)
     xd, out = _run(layer, x, ei)
     _check_grads(layer, state, xd, out, ei, x, H, concat, gout)
+
+
+@pytest.mark.parametrize("n,hf,fin", [(5000, 64, 602), (3001, 64, 50), (777, 8, 3), (1000, 32, 128),
+                                      (513, 128, 7), (64, 48, 33), (1, 64, 602)])
+def test_input_grad_kernel_vs_float64(n, hf, fin):
+    """gat_input_grad (dx = dWh W, the hand-written matrix-core kernel that
+    replaced torch.mm) against a float64 product, at fp32 tolerance."""
+    from atmlgraphattentionnetworks_amd import _lib
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(n + hf + fin)
+    dwh = torch.randn(n, hf, generator=g).to(dev)
+    w = torch.randn(hf, fin, generator=g).to(dev)
+    dx = torch.full((n, fin), float("nan"), device=dev)
+    rc = _lib.load().gat_input_grad(dwh.data_ptr(), hf, n, hf, w.data_ptr(), fin, dx.data_ptr(),
+                                    fin, torch._C._cuda_getCurrentRawStream(0))
+    assert rc == 0
+    torch.cuda.synchronize()
+    ref = dwh.double().cpu() @ w.double().cpu()
+    err = (dx.double().cpu() - ref).abs().max().item()
+    assert err <= 1e-5 * max(1.0, ref.abs().max().item()), err
