@@ -1,0 +1,12 @@
+#!/bin/bash
+# wres direct epilogue: parity + arxiv projection A/B + bench arxiv
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+TAG=${1:-r03u}
+mkdir -p gpurun_out
+PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 400 $PYT -m gpu tests/test_gpu_parity.py tests/test_gpu_fullsize.py > gpurun_out/pytest_${TAG}.log 2>&1 &&
+timeout -k 10 300 python3 tools/proj_ab.py --workload arxiv --variants "base;GAT_PROJ_WK_DIRECT=0" > gpurun_out/proj_ab_arxiv_${TAG}.json 2>&1 &&
+timeout -k 10 300 python3 bench.py --workload arxiv --workloads '' --no-pmc --no-train --no-cpu-baseline --emulate-ranks '' > gpurun_out/bench_arxiv_${TAG}.json 2> gpurun_out/bench_arxiv_${TAG}.err
+echo "chain exit $?"
