@@ -566,6 +566,102 @@ __global__ __launch_bounds__(256) void k_project_pipe2(
 }
 
 // ---------------------------------------------------------------------------
+// Direct projection epilogue (the projection kernels' DIRECT form).  The MFMA
+// operands are swapped (A = W fragment, B = x fragment), so the accumulators
+// hold Wh^T: lane l (kq = l >> 4) has Wh[row][16t + 4kq .. +4] of its tile
+// row, four consecutive columns.  Wh leaves as float4s straight from the
+// registers; each head's scores s = Wh_h.a_h + c_h (GAT.py:44-45) are xor
+// sums over the head's F/4 lanes.  For 8 heads of 8 (every reference
+// configuration's first layer) a row's eight scores are gathered into one lane
+// by two shuffles and stored as float4s: one contiguous 512-B run per wave
+// instead of four instructions of scattered 4-B stores (PPI projection 8.2 ->
+// 7.5 us).  Parameters: per column bs (Linear bias), a1s, a2s; per head c1s,
+// c2s (16-B aligned, typically in LDS).
+// ---------------------------------------------------------------------------
+template <int NT>
+__device__ __forceinline__ void proj_direct_epilogue(
+    const f32x4 (&acc)[NT], int row, int n, int kq, const float* bs, const float* a1s,
+    const float* a2s, const float* c1s, const float* c2s, int H, int F, int HF,
+    float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
+    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt) {
+    const int hfp = round_up4(HF);
+    const int hl = F >> 2;  // lanes (kq) per head: 1, 2 or 4
+    if constexpr (NT == 4) {
+        if (H == 8 && F == 8) {
+            // after the pair sums, lanes kq 0/1 hold head 2t and kq 2/3 head
+            // 2t + 1 of tile t; lane kq 0 (kq 1) gathers heads 0-3 (4-7) of its
+            // row from its kq ^ 2 partner
+            float s1[NT], s2[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int c0 = 16 * t + 4 * kq;
+                const f32x4 v = acc[t] + *reinterpret_cast<const f32x4*>(bs + c0);
+                const f32x4 q1 = *reinterpret_cast<const f32x4*>(a1s + c0);
+                const f32x4 q2 = *reinterpret_cast<const f32x4*>(a2s + c0);
+                const float p1 = v.x * q1.x + v.y * q1.y + v.z * q1.z + v.w * q1.w;
+                const float p2 = v.x * q2.x + v.y * q2.y + v.z * q2.z + v.w * q2.w;
+                s1[t] = p1 + __shfl_xor(p1, 16);
+                s2[t] = p2 + __shfl_xor(p2, 16);
+                if (row < n) {
+                    const int g = c0 / slice_w;
+                    store_out4(Wh, (size_t)g * (size_t)slice_stride + (size_t)row * ld_wh +
+                                       (c0 - g * slice_w), v, store_wt);
+                }
+            }
+            float o1[NT], o2[NT];  // the kq ^ 2 partner's heads (2t + 1 for kq < 2)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                o1[t] = __shfl_xor(s1[t], 32);
+                o2[t] = __shfl_xor(s2[t], 32);
+            }
+            if (kq < 2 && row < n) {
+                // kq 0: heads 0-3 = tiles 0, 1; kq 1: heads 4-7 = tiles 2, 3
+                const f32x4 cs2 = *reinterpret_cast<const f32x4*>(c2s + 4 * kq);
+                store_out4(s_dst, (size_t)row * 8 + 4 * kq,
+                           f32x4{kq ? s2[2] : s2[0], kq ? o2[2] : o2[0],
+                                 kq ? s2[3] : s2[1], kq ? o2[3] : o2[1]} + cs2, store_wt);
+                if (Ss != nullptr) {
+                    const f32x4 cs1 = *reinterpret_cast<const f32x4*>(c1s + 4 * kq);
+                    const f32x4 v1 = f32x4{kq ? s1[2] : s1[0], kq ? o1[2] : o1[0],
+                                           kq ? s1[3] : s1[1], kq ? o1[3] : o1[1]} + cs1;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        store_out1(Ss, (size_t)row * ld_s + 4 * kq + i, v1[i], store_wt);
+                }
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int c0 = 16 * t + 4 * kq;
+        const f32x4 v = acc[t] + *reinterpret_cast<const f32x4*>(bs + c0);
+        const f32x4 q1 = *reinterpret_cast<const f32x4*>(a1s + c0);
+        const f32x4 q2 = *reinterpret_cast<const f32x4*>(a2s + c0);
+        float p1 = v.x * q1.x + v.y * q1.y + v.z * q1.z + v.w * q1.w;
+        float p2 = v.x * q2.x + v.y * q2.y + v.z * q2.z + v.w * q2.w;
+        if (hl >= 2) {
+            p1 += __shfl_xor(p1, 16);
+            p2 += __shfl_xor(p2, 16);
+        }
+        if (hl >= 4) {
+            p1 += __shfl_xor(p1, 32);
+            p2 += __shfl_xor(p2, 32);
+        }
+        if (row < n && c0 < hfp) {
+            const int g = c0 / slice_w;  // slice_w % 4 == 0: one plane per float4
+            store_out4(Wh, (size_t)g * (size_t)slice_stride + (size_t)row * ld_wh +
+                               (c0 - g * slice_w), v, store_wt);
+            if ((kq & (hl - 1)) == 0 && c0 < HF) {
+                const int h = c0 / F;
+                if (Ss != nullptr) store_out1(Ss, (size_t)row * ld_s + h, p1 + c1s[h], store_wt);
+                store_out1(s_dst, (size_t)row * H + h, p2 + c2s[h], store_wt);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Projection on the bf16 matrix cores with split operands (Fin > 64: arxiv,
 // Reddit).  gfx950's fp32 MFMA runs at the fp32 vector rate (1/16 of bf16), so
 // the fp32 kernel above is MFMA-bound at Reddit scale (18 GFLOP: 115 us at
@@ -1188,84 +1284,9 @@ __global__ __launch_bounds__(256) void k_project_wk(
         }
     }
     if constexpr (DIRECT) {
-        // lane: row w*16 + cl, columns c0 = 16t + 4kq .. +4 of every tile t
-        const int row = row0 + w * 16 + cl;
-        const int hfp = round_up4(HF);
-        const int hl = F >> 2;  // lanes (kq) per head: 1, 2 or 4
-        if constexpr (NT == 4) if (H == 8 && F == 8) {
-            // 8 heads of 8 (every reference configuration's layer 1): after the
-            // pair sums, lanes kq 0/1 hold heads 2t and kq 2/3 heads 2t + 1 of
-            // tile t; lane kq 0 (kq 1) gathers heads 0-3 (4-7) of its row from
-            // its kq ^ 2 partner and stores them as ONE float4, so a wave
-            // writes its 16 rows' scores as one contiguous 512-B run instead of
-            // four instructions of scattered 4-B stores
-            float s1[NT], s2[NT];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const int c0 = 16 * t + 4 * kq;
-                const f32x4 v = acc[t] + *reinterpret_cast<const f32x4*>(bs + c0);
-                const f32x4 q1 = *reinterpret_cast<const f32x4*>(a1s + c0);
-                const f32x4 q2 = *reinterpret_cast<const f32x4*>(a2s + c0);
-                float p1 = v.x * q1.x + v.y * q1.y + v.z * q1.z + v.w * q1.w;
-                float p2 = v.x * q2.x + v.y * q2.y + v.z * q2.z + v.w * q2.w;
-                s1[t] = p1 + __shfl_xor(p1, 16);
-                s2[t] = p2 + __shfl_xor(p2, 16);
-                if (row < n) {
-                    const int g = c0 / slice_w;
-                    store_out4(Wh, (size_t)g * (size_t)slice_stride + (size_t)row * ld_wh +
-                                       (c0 - g * slice_w), v, store_wt);
-                }
-            }
-            float o1[NT], o2[NT];  // the kq ^ 2 partner's heads (2t + 1 for kq < 2)
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                o1[t] = __shfl_xor(s1[t], 32);
-                o2[t] = __shfl_xor(s2[t], 32);
-            }
-            if (kq < 2 && row < n) {
-                // kq 0: heads 0-3 = tiles 0, 1; kq 1: heads 4-7 = tiles 2, 3
-                const f32x4 cs2 = *reinterpret_cast<const f32x4*>(c2s + 4 * kq);
-                store_out4(s_dst, (size_t)row * 8 + 4 * kq,
-                           f32x4{kq ? s2[2] : s2[0], kq ? o2[2] : o2[0],
-                                 kq ? s2[3] : s2[1], kq ? o2[3] : o2[1]} + cs2, store_wt);
-                if (Ss != nullptr) {
-                    const f32x4 cs1 = *reinterpret_cast<const f32x4*>(c1s + 4 * kq);
-                    const f32x4 v1 = f32x4{kq ? s1[2] : s1[0], kq ? o1[2] : o1[0],
-                                           kq ? s1[3] : s1[1], kq ? o1[3] : o1[1]} + cs1;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        store_out1(Ss, (size_t)row * ld_s + 4 * kq + i, v1[i], store_wt);
-                }
-            }
-            return;
-        }
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int c0 = 16 * t + 4 * kq;
-            const f32x4 v = acc[t] + *reinterpret_cast<const f32x4*>(bs + c0);
-            const f32x4 q1 = *reinterpret_cast<const f32x4*>(a1s + c0);
-            const f32x4 q2 = *reinterpret_cast<const f32x4*>(a2s + c0);
-            float p1 = v.x * q1.x + v.y * q1.y + v.z * q1.z + v.w * q1.w;
-            float p2 = v.x * q2.x + v.y * q2.y + v.z * q2.z + v.w * q2.w;
-            if (hl >= 2) {
-                p1 += __shfl_xor(p1, 16);
-                p2 += __shfl_xor(p2, 16);
-            }
-            if (hl >= 4) {
-                p1 += __shfl_xor(p1, 32);
-                p2 += __shfl_xor(p2, 32);
-            }
-            if (row < n && c0 < hfp) {
-                const int g = c0 / slice_w;  // slice_w % 4 == 0: one plane per float4
-                store_out4(Wh, (size_t)g * (size_t)slice_stride + (size_t)row * ld_wh +
-                                   (c0 - g * slice_w), v, store_wt);
-                if ((kq & (hl - 1)) == 0 && c0 < HF) {
-                    const int h = c0 / F;
-                    if (Ss != nullptr) store_out1(Ss, (size_t)row * ld_s + h, p1 + c1s[h], store_wt);
-                    store_out1(s_dst, (size_t)row * H + h, p2 + c2s[h], store_wt);
-                }
-            }
-        }
+        proj_direct_epilogue<NT>(acc, row0 + w * 16 + cl, n, kq, bs, a1s, a2s, c1s, c2s, H, F,
+                                 HF, Wh, ld_wh, Ss, ld_s, s_dst, slice_w, slice_stride,
+                                 store_wt);
         return;
     }
     __syncthreads();  // X/W tiles dead: reuse LDS for the output tile

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-rank compute of the partitioned step (distributed.emulate_rank_times)
+under kernel knobs, on one GPU: which edge-kernel schedule suits a rank's
+small share of a graph?
+
+    python3 tools/emu_probe.py --workload ppi --ranks 8 --variants "base;GAT_EDGE_U=8"
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from atmlgraphattentionnetworks_amd import tuning  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="ppi")
+    ap.add_argument("--ranks", default="2,4,8")
+    ap.add_argument("--variants", default="base")
+    ap.add_argument("--exchange", default="allgather")
+    args = ap.parse_args()
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    from atmlgraphattentionnetworks_amd.distributed import emulate_rank_times
+    from atmlgraphattentionnetworks_amd.graph import build_csr
+    from atmlgraphattentionnetworks_amd.synthetic import WORKLOADS, make_inputs
+    dev = torch.device("cuda", 0)
+    w = WORKLOADS[args.workload]
+    x, ei = make_inputs(w, dev)
+    csr = build_csr(ei, x.size(0))
+    torch.manual_seed(0)
+    layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
+                                concat=w.concat).to(dev).eval()
+    knobs = set()
+    variants = []
+    for spec in args.variants.split(";"):
+        env = {} if spec in ("", "base") else dict(kv.split("=", 1) for kv in spec.split(","))
+        knobs |= set(env)
+        variants.append((spec, env))
+    out = {}
+    with torch.no_grad():
+        for spec, env in variants:
+            for k in knobs:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            tuning.reload()
+            for p in [int(v) for v in args.ranks.split(",")]:
+                r = emulate_rank_times(layer, csr, x, p, exchange=args.exchange)
+                out[f"{spec}|P{p}"] = {"max_project_us": r["max_project_ms"] * 1e3,
+                                       "max_edge_passes_us": r["max_edge_passes_ms"] * 1e3,
+                                       "chunks": r["chunks"]}
+    print(json.dumps({"workload": args.workload, "exchange": args.exchange, "results": out},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()

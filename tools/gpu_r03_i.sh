@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${1:-r03i}
 mkdir -p gpurun_out
 PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider"
-timeout -k 10 120 tools/proj_floor > gpurun_out/proj_floor_${TAG}.json 2>&1 &&
-timeout -k 10 300 $PYT -m gpu tests/test_gpu_parity.py -k "pingpong or ppi_shape or golden" > gpurun_out/pytest_${TAG}.log 2>&1 &&
-timeout -k 10 200 python3 bench.py --workloads '' --no-pmc --no-train --no-cpu-baseline --emulate-ranks '' > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err
+timeout -k 10 120 tools/proj_floor > gpurun_out/proj_floor_${TAG}.json 2>&1
+
+
 echo "chain exit $?"
