@@ -1558,7 +1558,14 @@ EdgeRows rows_of_csr(const int* rowptr) {
 // is then dy_i.Q_i - delta_i R_i: an elementwise kernel (k_bwd_table) instead of
 // a second pass over every in-edge (k_bwd_targets).  Q and R cost one more
 // accumulator per float4 and no gathers: the loop already holds Wh_j and p_ij.
-template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false>
+// S = 2 (short rows, few rows per launch): TWO lane groups per row, each
+// walking every other chunk of the row's in-edges (half 0 chunks 0, 2, 4, ...,
+// half 1 chunks 1, 3, ...); at the end each lane merges its online-softmax
+// state with its partner's (lane ^ G): M = max(m, m'), l = l 2^(m-M) + l'
+// 2^(m'-M), acc likewise (the hub merge, in registers).  The chain of
+// dependent chunk loads per row halves and a launch has twice the waves.
+// Only half 0 stores.  Not with KINK or PIPE.
+template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -1570,6 +1577,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     int nslices, int slice_w, long long slice_stride, float* __restrict__ q_heads,
     float* __restrict__ r_heads, int store_wt) {
     const DropArgs drop = resolve_drop(drop_arg);
+    static_assert(S == 1 || (S == 2 && !KINK && !PIPE && G * S <= kWave), "split rows");
     // col values held per lane per chunk.  Groups of >= 4 lanes: every quad of
     // the group holds the chunk's indices (lane c: edges (c & 3) + 4t), so the
     // source ids are broadcast by DPP within the quad instead of LDS permutes
@@ -1585,8 +1593,9 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     // only — an [N, slice_w] plane small enough to stay in that XCD's L2
     const int sl = nslices > 1 ? (int)(blockIdx.x % (unsigned)nslices) : 0;
     const unsigned blk = nslices > 1 ? blockIdx.x / (unsigned)nslices : blockIdx.x;
-    const int pos = row_begin + (int)((blk * (size_t)blockDim.x + threadIdx.x) / G);
+    const int pos = row_begin + (int)((blk * (size_t)blockDim.x + threadIdx.x) / (G * S));
     if (pos >= row_end) return;
+    const int half = S == 2 ? (lane / G) & 1 : 0;  // S = 2: which chunks of the row
     const int r = order != nullptr ? order[pos] : pos;
     const int sw = nslices > 1 ? slice_w : HF;  // columns this block's groups own
     const bool c_ok = 4 * V * c < sw;
@@ -1624,7 +1633,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     float lc = 0.f, racc = 0.f, rc = 0.f;
 #pragma unroll
     for (int q = 0; q < V; ++q) acc[q] = cmp[q] = accq[q] = cmpq[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (er.load) {  // continue a row whose earlier segments a previous pass ran
+    if (er.load && half == 0) {  // continue a row whose earlier segments a previous pass ran
         m = er.st_ml[(size_t)si * 2 * H + h];
         l = er.st_ml[(size_t)si * 2 * H + H + h];
         if (c_ok) {
@@ -1640,7 +1649,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
     // an empty row (possible only through a caller-built CSR: gat_csr_build adds a
     // self-loop to every row) loads nothing and stores the bias
-    for (int t = 0; t < CL; ++t) cv[t] = e1 > e0 ? col[min(e0 + cfirst + t * cstep, e1 - 1)] : 0;
+    for (int t = 0; t < CL; ++t)
+        cv[t] = e1 > e0 ? col[min(e0 + half * U + cfirst + t * cstep, e1 - 1)] : 0;
     // gathers of one chunk: source ids broadcast from the group's col values
     auto fetch = [&](const int (&cc)[CL], f32x4 (&v)[U][V], float (&s)[U]) {
         int j[U];
@@ -1808,10 +1818,10 @@ __global__ __launch_bounds__(256) void k_edge_grp(
             for (int t = 0; t < CL; ++t) cn[t] = cnn[t];
         }
     } else {
-        for (int k = e0; k < e1; k += U) {
+        for (int k = e0 + half * U; k < e1; k += S * U) {
             int cn[CL];
 #pragma unroll
-            for (int t = 0; t < CL; ++t) cn[t] = col[min(k + U + cfirst + t * cstep, e1 - 1)];
+            for (int t = 0; t < CL; ++t) cn[t] = col[min(k + S * U + cfirst + t * cstep, e1 - 1)];
             f32x4 v[U][V];
             float s[U];
             fetch(cv, v, s);
@@ -1819,6 +1829,36 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
             for (int t = 0; t < CL; ++t) cv[t] = cn[t];
         }
+    }
+    if constexpr (S == 2) {
+        // merge the two halves' states (both halves end with the same values:
+        // a + b == b + a exactly); the Kahan compensation is applied first
+        if (kahan) {
+            l -= lc;
+            lc = 0.f;
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                acc[q] -= cmp[q];
+                cmp[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+        const float mp = __shfl_xor(m, G), lp = __shfl_xor(l, G);
+        const float mm = fmaxf(m, mp);
+        // an empty half (fewer than U + 1 edges) has m = -inf and contributes 0
+        const float so = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - mm);
+        const float sp = mp == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mp - mm);
+        l = l * so + lp * sp;
+#pragma unroll
+        for (int q = 0; q < V; ++q) {
+            f32x4 ap;
+            ap.x = __shfl_xor(acc[q].x, G);
+            ap.y = __shfl_xor(acc[q].y, G);
+            ap.z = __shfl_xor(acc[q].z, G);
+            ap.w = __shfl_xor(acc[q].w, G);
+            acc[q] = acc[q] * so + ap * sp;
+        }
+        m = mm;
+        if (half != 0) return;
     }
 
     if (pos < er.store_lt) {  // a segment: hand the state on (the row is not finished)
@@ -2929,7 +2969,7 @@ const char* const kKnobNames[] = {
     "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
     "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
     "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS", "GAT_BWD_KINK",
-    "GAT_WGRAD_LW",    "GAT_STORE_WT",    "GAT_PROJ_WK_DIRECT"};
+    "GAT_WGRAD_LW",    "GAT_STORE_WT",    "GAT_PROJ_WK_DIRECT", "GAT_EDGE_SPLIT"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -3199,7 +3239,8 @@ int gat_project_sliced(const float* x, int n, int fin, const float* w, const flo
 // chunk ahead (GAT_EDGE_PIPE A/B knob): instantiated for the (U, V) pairs the
 // default schedule uses.
 template <int G, int U, int V, bool KINK = false, class... A>
-static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A... a) {
+static void launch_edge_fused(int pipe, int split, dim3 grid, dim3 block, hipStream_t st,
+                              A... a) {
     // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
     // kernel — caps the blocks resident per CU (160 KB / bytes)
     size_t lds = 0;
@@ -3209,6 +3250,15 @@ static void launch_edge_fused(int pipe, dim3 grid, dim3 block, hipStream_t st, A
     if constexpr (V == 2 && U == 16) {
         if (pipe) {
             hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true, KINK>), grid, block, lds, st, a...);
+            return;
+        }
+    }
+    // two lane groups per row (S = 2, GAT_EDGE_SPLIT): instantiated for the
+    // short-row lane groups of HF = 64 (G = 8: 2-plane table; G = 16: row-major)
+    if constexpr (!KINK && V == 1 && U <= 8 && (G == 8 || G == 16)) {
+        if (split == 2) {
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 2>),
+                               dim3(grid.x * 2), block, lds, st, a...);
             return;
         }
     }
@@ -3222,7 +3272,7 @@ static bool kink_grp_ok(int g, int v) { return (g == 16 && v == 1) || (g == 8 &&
 template <int G, int U, int V, class... A>
 static void launch_edge_kink(int pipe, dim3 grid, dim3 block, hipStream_t st, A... a) {
     if constexpr ((G == 16 && V == 1) || (G == 8 && V == 2))
-        launch_edge_fused<G, U, V, true>(pipe, grid, block, st, a...);
+        launch_edge_fused<G, U, V, true>(pipe, 1, grid, block, st, a...);
 }
 
 extern "C" {
@@ -3315,6 +3365,19 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // rows keep more, shallower waves (PPI 30.5 -> 32.9 us pipelined)
         int pipe = (u == 16 && vv == 2) ? 1 : 0;
         if (const char* ep = knob("GAT_EDGE_PIPE")) pipe = std::atoi(ep);
+        // two lane groups per row (the grid doubles inside launch_edge_fused):
+        // GAT_EDGE_SPLIT = 2 (A/B knob); rows that run segment passes (er.load /
+        // store_lt) and the kink-sum forward keep one group
+        // Default: launches of fewer than ~4 waves per SIMD (a rank's share of a
+        // small graph: PPI at P = 4 / 8 edge passes 14.4 -> 11.3 / 13.4 -> 9.4 us,
+        // tools/emu_probe.py) — there the per-row chain of dependent chunk loads
+        // is exposed; larger launches hide it and the split only adds work (full
+        // PPI 27.8 -> 30.8 us, arxiv 54.2 -> 61.2 us).
+        const long long waves = (long long)rows * g * nslices / kWave;
+        int split = waves < 4096 ? 2 : 1;
+        if (const char* es = knob("GAT_EDGE_SPLIT")) split = std::atoi(es) == 2 ? 2 : 1;
+        if (kink || pipe) split = 1;
+        if ((long long)blocks * split >= (1LL << 31)) split = 1;
         if (kink && !kink_grp_ok(g, vv)) return GAT_EUNSUPPORTED;
 #define GAT_GRP_KARGS                                                                         \
     er, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,   \
@@ -3324,7 +3387,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     if (kink)                                                                         \
         launch_edge_kink<G, UU, VV>(pipe, grid, block, st, GAT_GRP_KARGS);             \
     else if (fused)                                                                   \
-        launch_edge_fused<G, UU, VV>(pipe, grid, block, st, GAT_GRP_KARGS);            \
+        launch_edge_fused<G, UU, VV>(pipe, split, grid, block, st, GAT_GRP_KARGS);     \
     else                                                                              \
         hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, GAT_GRP_KARGS)
 #define GAT_GRP_U(G, VV)                                                              \

@@ -37,6 +37,11 @@ VARIANTS = {
     "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds", "GAT_EDGE_SCHED": "0"},
     # the CSR-order launch (short rows take the scheduled copy by default)
     "nosched": {"GAT_EDGE_SCHED": "0"},
+    # two lane groups per row (short rows, U = 4/8, V = 1): forced on, and off
+    # (small test graphs take it by default)
+    "split2": {"GAT_EDGE_SPLIT": "2"},
+    "split1": {"GAT_EDGE_SPLIT": "1"},
+    "split2_u8_nosched": {"GAT_EDGE_SPLIT": "2", "GAT_EDGE_U": "8", "GAT_EDGE_SCHED": "0"},
     # projection: k_project_x3 for 64 < fin <= 128 (WRES=0), k_project_wres for
     # every fin <= 128, the tiled fallback; plain stores instead of write-through
     "proj_wk": {"GAT_PROJ_WRES": "0"},
@@ -56,7 +61,8 @@ def variant(request, monkeypatch):
     for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
-              "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT"):
+              "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
+              "GAT_EDGE_SPLIT"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -263,6 +269,9 @@ def test_sliced_table_equals_row_major(slices, H, F, fin, monkeypatch):
     n, e = 1500, 30000
     x, ei, state = random_case(n, e, fin, H, F, True, seed=slices * 100 + H)
     layer = layer_from_state(state, fin, F, H, True)
+    # one lane group per row in both layouts (the two-group split of small
+    # launches applies to some lane-group widths only, and regroups the sums)
+    monkeypatch.setenv("GAT_EDGE_SPLIT", "1")
     monkeypatch.setenv("GAT_WH_SLICES", str(slices))
     assert wh_slices(H, F, True, 0.2) == slices
     pp = layer.packed()

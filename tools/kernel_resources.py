@@ -31,15 +31,14 @@ def main():
     for blk in notes.split("  - .agpr_count:")[1:]:
         get = lambda k: (re.search(rf"\.{k}:\s+(\S+)", blk) or [None, "-"])[1]
         name = get("name")
-        if pats and not any(p in name for p in pats):
+        dem = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
+        if pats and not any(p in dem for p in pats):
             continue
-        rows.append((name, blk.split()[0], get("vgpr_count"), get("sgpr_count"),
+        rows.append((dem, blk.split()[0], get("vgpr_count"), get("sgpr_count"),
                      get("group_segment_fixed_size"), get("private_segment_fixed_size"),
                      get("vgpr_spill_count")))
     print(f"{'agpr':>4} {'vgpr':>4} {'sgpr':>4} {'lds':>6} {'scr':>4} {'spill':>5}  kernel")
-    for name, a, v, s, l, p, sp in sorted(rows):
-        dem = subprocess.run(["c++filt", name], capture_output=True,
-                             text=True).stdout.strip()
+    for dem, a, v, s, l, p, sp in sorted(rows):
         print(f"{a:>4} {v:>4} {s:>4} {l:>6} {p:>4} {sp:>5}  {dem[:150]}")
 
 
