@@ -18,7 +18,7 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 6
+GAT_ABI_VERSION = 7
 GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
 GAT_SEG_LOAD = 1
 GAT_SEG_STORE = 2
@@ -90,6 +90,10 @@ SIGNATURES = {
     "gat_weight_grad_workspace_size": (_c_int, [_c_int, _c_int, _c_int, _c_size_p]),
     "gat_weight_grad": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_int, _c_int, _c_vp, _c_vp,
                                  ctypes.c_size_t, _c_vp]),
+    "gat_layer_forward": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                   _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
+                                   _c_vp, _c_vp, _c_vp, _c_int, _c_float, _c_vp, _c_vp, _c_int,
+                                   _c_vp]),
     "gat_input_grad": (_c_int, [_c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_int,
                                 _c_vp]),
     "gat_sum_partials_workspace_size": (_c_int, [_c_int, _c_ll, _c_size_p]),

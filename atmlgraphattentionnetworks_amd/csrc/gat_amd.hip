@@ -3528,6 +3528,39 @@ int gat_edge_aggregate_seg(const int* seg_begin, const int* seg_end, int seg_by_
                            const float* a_src, const float* c_src, const float* s_dst, int heads,
                            int f, int concat, float negative_slope, float* st_acc, float* st_ml,
                            int flags, int store_rows, const float* bias, float* out,
+                           int edges_per_row_hint, void* stream);
+
+// The eval forward in one call (gat_project[_sliced] into a caller-owned table,
+// then gat_edge_aggregate_seg over a scheduled CSR copy, rows by position):
+// the host enqueue of a small graph's forward is one C-ABI call, not two.
+int gat_layer_forward(const float* x, int n, int fin, const float* w, const float* b,
+                      const float* a_src, const float* c_src, const float* a_dst,
+                      const float* c_dst, int heads, int f, int slices, float* wh, float* s_src,
+                      float* s_dst, const int* seg_begin, const int* seg_end, const int* col,
+                      const int* row_order, int concat, float negative_slope, const float* bias,
+                      float* out, int edges_per_row_hint, void* stream) {
+    if (heads <= 0 || f <= 0 || slices <= 0 || n < 0) return GAT_EINVAL;
+    const int hf = heads * f, hfp = round_up4(hf);
+    int rc;
+    if (slices > 1)
+        rc = gat_project_sliced(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
+                                n, nullptr, heads, s_dst, stream);
+    else
+        rc = gat_project(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, wh, hfp, s_src,
+                         heads, s_dst, stream);
+    if (rc != GAT_OK) return rc;
+    return gat_edge_aggregate_seg(seg_begin, seg_end, 1, col, row_order, 0, n, wh,
+                                  slices > 1 ? hf / slices : hfp, n, slices, a_src, c_src, s_dst,
+                                  heads, f, concat, negative_slope, nullptr, nullptr, 0, 0, bias,
+                                  out, edges_per_row_hint, stream);
+}
+
+int gat_edge_aggregate_seg(const int* seg_begin, const int* seg_end, int seg_by_pos,
+                           const int* col, const int* row_order, int row_begin, int row_end,
+                           const float* wh, int ld_wh, int n_table, int slices,
+                           const float* a_src, const float* c_src, const float* s_dst, int heads,
+                           int f, int concat, float negative_slope, float* st_acc, float* st_ml,
+                           int flags, int store_rows, const float* bias, float* out,
                            int edges_per_row_hint, void* stream) {
     if (seg_begin == nullptr || seg_end == nullptr || a_src == nullptr || c_src == nullptr)
         return GAT_EINVAL;

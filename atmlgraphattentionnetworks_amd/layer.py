@@ -365,38 +365,29 @@ class ForwardPlan:
                 return self.edge(lib, self.csr, pp, bias, out)
             b = self.bound = self._bind(lib, pp, bias)
         stream = torch._C._cuda_getCurrentRawStream(self.dev)
-        rc = b[3](x.data_ptr(), *b[4][self.cur], stream)
+        # projection + edge kernel in one C-ABI call (gat_layer_forward)
+        rc = b[3](x.data_ptr(), *b[4][self.cur], out.data_ptr(), self.khint, stream)
         if rc:
             if rc == _lib.GAT_EUNSUPPORTED and self.slices > 1:
-                self.bound = None  # fall back to the row-major table (project() decides)
+                # the sliced projection launched nothing: fall back to the
+                # row-major table (project() decides)
+                self.bound = None
                 self.project(lib, x, pp)
                 return self.edge(lib, self.csr, pp, bias, out)
-            _lib.check(rc, "gat_project")
-        rc = b[6](*b[7][self.cur], out.data_ptr(), self.khint, stream)
-        if rc:
-            _lib.check(rc, "gat_edge_aggregate_seg (scheduled CSR)")
+            _lib.check(rc, "gat_layer_forward")
         return out
 
     def _bind(self, lib, pp: PackedParams, bias: torch.Tensor):
         n, fin, heads, f, sc = self.n, self.fin, self.heads, self.f, self.sched
         pw = (pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(), pp.c_src.data_ptr(),
               pp.a_dst.data_ptr(), pp.c_dst.data_ptr())
-        ld = self.hf // self.slices if self.slices > 1 else self.hfp
         p_order = 0 if self.csr.order is None else self.csr.order.data_ptr()
-        pargs, eargs = [], []
+        fargs = []
         for p_wh, p_ss, p_sd in self.bufs:  # one argument list per workspace
-            if self.slices > 1:
-                pfn = lib.gat_project_sliced
-                pargs.append((n, fin, *pw, heads, f, self.slices, p_wh, n, 0, heads, p_sd))
-            else:
-                pfn = lib.gat_project
-                pargs.append((n, fin, *pw, heads, f, p_wh, self.hfp, p_ss, heads, p_sd))
-            eargs.append((sc.b.data_ptr(), sc.e.data_ptr(), 1, sc.col.data_ptr(), p_order, 0, n,
-                          p_wh, ld, n, self.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
-                          p_sd, heads, f, int(self.concat), self.slope, 0, 0, 0, 0,
-                          bias.data_ptr()))
-        return (pp, bias.data_ptr(), lib, pfn, pargs, self.slices > 1,
-                lib.gat_edge_aggregate_seg, eargs)
+            fargs.append((n, fin, *pw, heads, f, self.slices, p_wh, p_ss, p_sd, sc.b.data_ptr(),
+                          sc.e.data_ptr(), sc.col.data_ptr(), p_order, int(self.concat),
+                          self.slope, bias.data_ptr()))
+        return (pp, bias.data_ptr(), lib, lib.gat_layer_forward, fargs, self.slices > 1)
 
     def project(self, lib, x: torch.Tensor, pp: PackedParams) -> None:
         """gat_project(_sliced) into the workspace (GAT.py:42-52)."""

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 6
+#define GAT_ABI_VERSION 7
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -215,6 +215,22 @@ int gat_edge_aggregate_seg(const int* seg_begin, const int* seg_end, int seg_by_
 int gat_edge_merge(const int* hub_rows, const int* seg_ptr, int n_hub, const float* st_acc,
                    const float* st_ml, int heads, int f, int concat, const float* bias,
                    float* out, float* lse, float* y_heads, void* stream);
+
+/*
+ * The eval forward in one call: gat_project (slices == 1: row-major Wh at
+ * ld = round_up(heads*f, 4), s_src [n, heads]) or gat_project_sliced (slices > 1,
+ * n_table = n, s_src unused), then gat_edge_aggregate_seg over a scheduled CSR
+ * copy (seg_by_pos = 1: position p covers col[seg_begin[p] .. seg_end[p]) of
+ * target row_order[p]; rows 0 .. n).  Replaces GAT.py:37-67 + GAT.py:54 for a
+ * graph whose self-loops are already in the CSR.  Returns the first failing
+ * call's status (GAT_EUNSUPPORTED from the projection launches nothing).
+ */
+int gat_layer_forward(const float* x, int n, int fin, const float* w, const float* b,
+                      const float* a_src, const float* c_src, const float* a_dst,
+                      const float* c_dst, int heads, int f, int slices, float* wh, float* s_src,
+                      float* s_dst, const int* seg_begin, const int* seg_end, const int* col,
+                      const int* row_order, int concat, float negative_slope, const float* bias,
+                      float* out, int edges_per_row_hint, void* stream);
 
 /* Workspace bytes gat_csr_build needs for (num_edges, num_nodes). */
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);
