@@ -158,7 +158,7 @@ def _act_module(name):
 
 
 def _worker(rank, world, port, exchange, concat, results, F=8, slices=None, chunks=None,
-            act=None):
+            act=None, repeat=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if slices is not None:
         os.environ["GAT_WH_SLICES"] = str(slices)
@@ -179,6 +179,22 @@ def _worker(rank, world, port, exchange, concat, results, F=8, slices=None, chun
         out = sh.forward(sh.local_x(x))
         full = gather_output(out, sh.bounds)
         results["fused"] = sh.fused
+        if repeat:
+            # forward() alternates two node tables (pingpong): another x, then x
+            # again, must give each input's own result
+            tables = [t.data_ptr() for t in sh.tables]
+            used = [sh.table.data_ptr()]
+            x2 = torch.randn_like(x)
+            full2 = gather_output(sh.forward(sh.local_x(x2)).clone(), sh.bounds)
+            used.append(sh.table.data_ptr())
+            full3 = gather_output(sh.forward(sh.local_x(x)).clone(), sh.bounds)
+            used.append(sh.table.data_ptr())
+            results["tables_alternate"] = (len(set(tables)) == 2 and used[0] != used[1]
+                                           and used[0] == used[2])
+            results["repeat_equal"] = bool(torch.equal(full3, full))
+            if rank == 0:
+                ref2 = gat_layer_forward_from_state(state, x2, ei, H, concat)
+                results["max_diff2"] = float((full2 - ref2).abs().max())
         if rank == 0:
             if module is None:
                 ref = gat_layer_forward_from_state(state, x, ei, H, concat)
@@ -324,3 +340,16 @@ def test_default_chunks_same_on_every_rank(monkeypatch):
             for r in range(world)]
     assert all(lay == lays[0] for lay in lays)
     assert lays[0].chunks == D.default_chunks(world, csr.num_edges, True)
+
+
+@pytest.mark.parametrize("exchange", ["allgather", "replicate"])
+def test_sharded_forward_repeated_pingpong(exchange):
+    """Back-to-back forwards of the sharded layer alternate its two node tables
+    and each gives its own input's result."""
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), exchange, True, results, 8, None, None, None, True),
+             nprocs=2, join=True)
+    assert results["tables_alternate"]
+    assert results["repeat_equal"]
+    assert results["max_diff"] < 1e-5 and results["max_diff2"] < 1e-5
