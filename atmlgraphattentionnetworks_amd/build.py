@@ -1,20 +1,32 @@
 """In-tree build of libgat_amd.so for gfx950 (no JIT cache: the .so travels
 with the repo snapshot to the GPU box).
 
+The library is five HIP translation units (csrc/*.hip, sharing
+csrc/gat_common.h); each compiles to an object under build/obj in its own
+hipcc process, in parallel, and one link makes the shared library.  Objects
+are rebuilt when their source, the shared header or include/gat_amd.h is
+newer.
+
     python -m atmlgraphattentionnetworks_amd.build [--force]
 """
 from __future__ import annotations
 
+import glob
 import os
 import subprocess
 import sys
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-SRC = os.path.join(PKG, "csrc", "gat_amd.hip")
+CSRC = os.path.join(PKG, "csrc")
+SRCS = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+COMMON = os.path.join(CSRC, "gat_common.h")
 HDR = os.path.join(ROOT, "include", "gat_amd.h")
+OBJ = os.path.join(ROOT, "build", "obj")
 LIB = os.path.join(PKG, "libgat_amd.so")
 ARCH = os.environ.get("GAT_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+         "-munsafe-fp-atomics"]
 
 
 def hipcc() -> str:
@@ -22,18 +34,35 @@ def hipcc() -> str:
     return os.path.join(rocm, "bin", "hipcc")
 
 
+def _stale(target: str, deps: list[str]) -> bool:
+    return (not os.path.exists(target)
+            or os.path.getmtime(target) < max(os.path.getmtime(d) for d in deps))
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
-    deps = [SRC, HDR]
-    if (not force and os.path.exists(LIB)
-            and os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps)):
-        return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-munsafe-fp-atomics",
-           "-o", LIB + ".tmp", SRC]
-    if verbose:
-        print("[build]", " ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
+    if not SRCS:
+        raise RuntimeError(f"no HIP sources under {CSRC}")
+    os.makedirs(OBJ, exist_ok=True)
+    objs, jobs = [], []
+    for src in SRCS:
+        obj = os.path.join(OBJ, os.path.basename(src)[:-4] + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src, COMMON, HDR]):
+            cmd = [hipcc(), f"--offload-arch={ARCH}", *FLAGS, "-c", "-o", obj + ".tmp", src]
+            if verbose:
+                print("[build]", " ".join(cmd), flush=True)
+            jobs.append((obj, subprocess.Popen(cmd)))
+    failed = [obj for obj, p in jobs if p.wait() != 0]
+    if failed:
+        raise RuntimeError("hipcc failed for " + ", ".join(os.path.basename(o) for o in failed))
+    for obj, _ in jobs:
+        os.replace(obj + ".tmp", obj)
+    if force or jobs or _stale(LIB, objs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
+        if verbose:
+            print("[build]", " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(LIB + ".tmp", LIB)
     return LIB
 
 

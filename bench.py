@@ -53,7 +53,7 @@ SPLIT_PRODUCTS = 6  # bf16 MFMA products per fp32 product in the split-bf16 proj
 
 
 def projection_kernel(fin: int) -> dict:
-    """The projection kernel the library picks for this Fin (gat_amd.hip
+    """The projection kernel the library picks for this Fin (gat_project.hip
     project_impl, default knobs) and the matrix dtype it issues."""
     if fin <= 64:
         return {"kernel": "k_project_wk", "mfma": "fp32 (v_mfma_f32_16x16x4_f32)",

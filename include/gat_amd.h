@@ -1,6 +1,6 @@
 /*
  * gat_amd.h — C-ABI of the MI355X (gfx950) GAT attention-layer library
- * (libgat_amd.so, built from atmlgraphattentionnetworks_amd/csrc/gat_amd.hip).
+ * (libgat_amd.so, built from the HIP sources in atmlgraphattentionnetworks_amd/csrc).
  *
  * Drop-in boundary for the hot path of danieldritter/ATMLGraphAttentionNetworks:
  * GraphAttentionLayer.forward(x, edge_index), GAT.py:37-67, and the PyG calls it

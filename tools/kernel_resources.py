@@ -20,13 +20,15 @@ def main():
     with tempfile.TemporaryDirectory() as d:
         subprocess.run([f"{LLVM}/llvm-objdump", "--offloading", LIB], cwd=d, check=True,
                        capture_output=True)
-        # the bundle is written next to the input: move it into the temp dir
+        # the bundles are written next to the input: move it into the temp dir
         for f in os.listdir(os.path.dirname(LIB)):
-            if f.startswith("libgat_amd.so.0."):
+            if re.match(r"libgat_amd\.so\.\d+\.", f):
                 os.replace(os.path.join(os.path.dirname(LIB), f), os.path.join(d, f))
-        co = [f for f in os.listdir(d) if "gfx950" in f][0]
-        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", os.path.join(d, co)],
-                               capture_output=True, text=True, check=True).stdout
+        # one code object per translation unit (csrc/*.hip)
+        notes = "".join(
+            subprocess.run([f"{LLVM}/llvm-readelf", "--notes", os.path.join(d, co)],
+                           capture_output=True, text=True, check=True).stdout
+            for co in sorted(os.listdir(d)) if "gfx950" in co)
     rows = []
     for blk in notes.split("  - .agpr_count:")[1:]:
         get = lambda k: (re.search(rf"\.{k}:\s+(\S+)", blk) or [None, "-"])[1]
