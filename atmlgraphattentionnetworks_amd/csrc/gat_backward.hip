@@ -720,11 +720,6 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dwh, in
     }
 }
 
-// out[b * width + e] = sum_c part[c * width + e] over rows c of row block
-// b = blockIdx.y ([b * rows_per_block, ...) ∩ [0, rows)): 16 columns x 16 row
-// groups per block, 4 independent loads in flight per thread, then a fixed
-// order combine in LDS (deterministic).  Sums the per-chunk / per-wave
-// partials of k_wgrad and k_src_bwd.
 // ---------------------------------------------------------------------------
 // Input gradient of the projection: dx[n, fin] = dWh[n, hf] W[hf, fin] (the x
 // side of GAT.py:42-48's Linear layers; replaces the hipBLASLt GEMM).  fp32
@@ -786,6 +781,11 @@ __global__ __launch_bounds__(256) void k_dx(const float* __restrict__ dwh, int l
     }
 }
 
+// out[b * width + e] = sum_c part[c * width + e] over rows c of row block
+// b = blockIdx.y ([b * rows_per_block, ...) ∩ [0, rows)): 16 columns x 16 row
+// groups per block, 4 independent loads in flight per thread, then a fixed
+// order combine in LDS (deterministic).  Sums the per-chunk / per-wave
+// partials of k_wgrad and k_src_bwd.
 __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ part, int rows,
                                                 long long width, float* __restrict__ out,
                                                 int rows_per_block) {

@@ -204,13 +204,13 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 // is then dy_i.Q_i - delta_i R_i: an elementwise kernel (k_bwd_table) instead of
 // a second pass over every in-edge (k_bwd_targets).  Q and R cost one more
 // accumulator per float4 and no gathers: the loop already holds Wh_j and p_ij.
-// S = 2 (short rows, few rows per launch): TWO lane groups per row, each
-// walking every other chunk of the row's in-edges (half 0 chunks 0, 2, 4, ...,
-// half 1 chunks 1, 3, ...); at the end each lane merges its online-softmax
-// state with its partner's (lane ^ G): M = max(m, m'), l = l 2^(m-M) + l'
-// 2^(m'-M), acc likewise (the hub merge, in registers).  The chain of
-// dependent chunk loads per row halves and a launch has twice the waves.
-// Only half 0 stores.  Not with KINK or PIPE.
+// S = 2 or 4 (short rows, few rows per launch): S lane groups per row, group
+// g walking chunks g, g + S, g + 2S, ... of the row's in-edges; at the end each
+// lane merges its online-softmax state with its partners' (lane ^ G, then
+// lane ^ 2G): M = max(m, m'), l = l 2^(m-M) + l' 2^(m'-M), acc likewise (the
+// hub merge, in registers).  The chain of dependent chunk loads per row is S
+// times shorter and a launch has S times the waves.  Only group 0 stores.
+// Not with KINK or PIPE.
 template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     int nslices, int slice_w, long long slice_stride, float* __restrict__ q_heads,
     float* __restrict__ r_heads, int store_wt) {
     const DropArgs drop = resolve_drop(drop_arg);
-    static_assert(S == 1 || (S == 2 && !KINK && !PIPE && G * S <= kWave), "split rows");
+    static_assert(S == 1 || ((S == 2 || S == 4) && !KINK && !PIPE && G * S <= kWave), "split rows");
     // col values held per lane per chunk.  Groups of >= 4 lanes: every quad of
     // the group holds the chunk's indices (lane c: edges (c & 3) + 4t), so the
     // source ids are broadcast by DPP within the quad instead of LDS permutes
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const unsigned blk = nslices > 1 ? blockIdx.x / (unsigned)nslices : blockIdx.x;
     const int pos = row_begin + (int)((blk * (size_t)blockDim.x + threadIdx.x) / (G * S));
     if (pos >= row_end) return;
-    const int half = S == 2 ? (lane / G) & 1 : 0;  // S = 2: which chunks of the row
+    const int half = S > 1 ? (lane / G) & (S - 1) : 0;  // S > 1: which chunks of the row
     const int r = order != nullptr ? order[pos] : pos;
     const int sw = nslices > 1 ? slice_w : HF;  // columns this block's groups own
     const bool c_ok = 4 * V * c < sw;
@@ -476,9 +476,10 @@ __global__ __launch_bounds__(256) void k_edge_grp(
             for (int t = 0; t < CL; ++t) cv[t] = cn[t];
         }
     }
-    if constexpr (S == 2) {
-        // merge the two halves' states (both halves end with the same values:
-        // a + b == b + a exactly); the Kahan compensation is applied first
+    if constexpr (S > 1) {
+        // merge the S groups' states by an xor butterfly over the groups (both
+        // partners of a step end with the same values: a + b == b + a exactly);
+        // the Kahan compensation is applied first
         if (kahan) {
             l -= lc;
             lc = 0.f;
@@ -488,22 +489,25 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 cmp[q] = f32x4{0.f, 0.f, 0.f, 0.f};
             }
         }
-        const float mp = __shfl_xor(m, G), lp = __shfl_xor(l, G);
-        const float mm = fmaxf(m, mp);
-        // an empty half (fewer than U + 1 edges) has m = -inf and contributes 0
-        const float so = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - mm);
-        const float sp = mp == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mp - mm);
-        l = l * so + lp * sp;
 #pragma unroll
-        for (int q = 0; q < V; ++q) {
-            f32x4 ap;
-            ap.x = __shfl_xor(acc[q].x, G);
-            ap.y = __shfl_xor(acc[q].y, G);
-            ap.z = __shfl_xor(acc[q].z, G);
-            ap.w = __shfl_xor(acc[q].w, G);
-            acc[q] = acc[q] * so + ap * sp;
+        for (int off = G; off < G * S; off <<= 1) {
+            const float mp = __shfl_xor(m, off), lp = __shfl_xor(l, off);
+            const float mm = fmaxf(m, mp);
+            // an empty group (a row shorter than its chunk) has m = -inf, adds 0
+            const float so = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - mm);
+            const float sp = mp == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mp - mm);
+            l = l * so + lp * sp;
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                f32x4 ap;
+                ap.x = __shfl_xor(acc[q].x, off);
+                ap.y = __shfl_xor(acc[q].y, off);
+                ap.z = __shfl_xor(acc[q].z, off);
+                ap.w = __shfl_xor(acc[q].w, off);
+                acc[q] = acc[q] * so + ap * sp;
+            }
+            m = mm;
         }
-        m = mm;
         if (half != 0) return;
     }
 
@@ -650,12 +654,18 @@ static void launch_edge_fused(int pipe, int split, dim3 grid, dim3 block, hipStr
             return;
         }
     }
-    // two lane groups per row (S = 2, GAT_EDGE_SPLIT): instantiated for the
-    // short-row lane groups of HF = 64 (G = 8: 2-plane table; G = 16: row-major)
+    // two or four lane groups per row (S = split, GAT_EDGE_SPLIT): instantiated
+    // for the short-row lane groups of HF = 64 (G = 8: 2-plane table; G = 16:
+    // row-major)
     if constexpr (!KINK && V == 1 && U <= 8 && (G == 8 || G == 16)) {
         if (split == 2) {
             hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 2>),
                                dim3(grid.x * 2), block, lds, st, a...);
+            return;
+        }
+        if (split == 4) {
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 4>),
+                               dim3(grid.x * 4), block, lds, st, a...);
             return;
         }
     }
@@ -772,7 +782,10 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // PPI 27.8 -> 30.8 us, arxiv 54.2 -> 61.2 us).
         const long long waves = (long long)rows * g * nslices / kWave;
         int split = waves < 4096 ? 2 : 1;
-        if (const char* es = knob("GAT_EDGE_SPLIT")) split = std::atoi(es) == 2 ? 2 : 1;
+        if (const char* es = knob("GAT_EDGE_SPLIT")) {
+            split = std::atoi(es);
+            if (split != 2 && split != 4) split = 1;
+        }
         if (kink || pipe) split = 1;
         if ((long long)blocks * split >= (1LL << 31)) split = 1;
         if (kink && !kink_grp_ok(g, vv)) return GAT_EUNSUPPORTED;

@@ -80,6 +80,28 @@ def test_sharded_hip_path_matches_oracle(P, exchange, concat, table, chunks, mon
     torch.testing.assert_close(full, ref, atol=ATOL, rtol=RTOL)
 
 
+@pytest.mark.parametrize("split", ["1", "2", "4"])
+@pytest.mark.parametrize("table", ["default", "row_major"])
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_sharded_split_rows_match_oracle(split, table, chunks, monkeypatch):
+    """GAT_EDGE_SPLIT: 1, 2 or 4 lane groups per row, merged in registers, in
+    the segment passes that carry (m, l, acc) across all-gather chunks."""
+    monkeypatch.setenv("GAT_EDGE_SPLIT", split)
+    if table == "row_major":
+        monkeypatch.setenv("GAT_WH_SLICES", "1")
+    else:
+        monkeypatch.delenv("GAT_WH_SLICES", raising=False)
+    from atmlgraphattentionnetworks_amd import get_csr
+    from atmlgraphattentionnetworks_amd.distributed import emulate
+    state, x, ei = _small_case(True)
+    layer = _layer(50, 8, 8, True, state)
+    csr = get_csr(ei, x.size(0))
+    with torch.no_grad():
+        full = emulate(layer, csr, x, 4, exchange="allgather", chunks=chunks).cpu()
+    ref = gat_layer_forward_from_state(state, x.cpu(), ei.cpu(), 8, True)
+    torch.testing.assert_close(full, ref, atol=ATOL, rtol=RTOL)
+
+
 @pytest.mark.parametrize("act_name,concat,chunks", [("lrelu0.3", True, 2), ("lrelu0.01", False, 3),
                                                     ("relu", True, 2), ("tanh", True, 1),
                                                     ("logsigmoid", False, 1)])

@@ -42,6 +42,8 @@ VARIANTS = {
     "split2": {"GAT_EDGE_SPLIT": "2"},
     "split1": {"GAT_EDGE_SPLIT": "1"},
     "split2_u8_nosched": {"GAT_EDGE_SPLIT": "2", "GAT_EDGE_U": "8", "GAT_EDGE_SCHED": "0"},
+    "split4": {"GAT_EDGE_SPLIT": "4"},
+    "split4_u8_nosched": {"GAT_EDGE_SPLIT": "4", "GAT_EDGE_U": "8", "GAT_EDGE_SCHED": "0"},
     # projection: k_project_x3 for 64 < fin <= 128 (WRES=0), k_project_wres for
     # every fin <= 128, the tiled fallback; plain stores instead of write-through
     "proj_wk": {"GAT_PROJ_WRES": "0"},
