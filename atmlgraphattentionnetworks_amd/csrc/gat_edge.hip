@@ -776,12 +776,16 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // GAT_EDGE_SPLIT = 2 (A/B knob); rows that run segment passes (er.load /
         // store_lt) and the kink-sum forward keep one group
         // Default: launches of fewer than ~4 waves per SIMD (a rank's share of a
-        // small graph: PPI at P = 4 / 8 edge passes 14.4 -> 11.3 / 13.4 -> 9.4 us,
+        // small graph: PPI at P = 4 / 8 edge passes 14.2 -> 11.3 / 13.3 -> 9.0 us,
         // tools/emu_probe.py) — there the per-row chain of dependent chunk loads
         // is exposed; larger launches hide it and the split only adds work (full
-        // PPI 27.8 -> 30.8 us, arxiv 54.2 -> 61.2 us).
+        // PPI 27.8 -> 30.8 us, arxiv 54.2 -> 61.2 us).  Four groups under ~2
+        // waves per SIMD (PPI at P = 8: 9.0 -> 8.2 us; at P = 4 it is 13.6).
+        // Rows of fewer than ~3 chunks per group gain nothing from a split (arxiv
+        // at P = 8, 8 edges per row: 10.9 us whole, 12.0 / 15.8 split 2 / 4).
         const long long waves = (long long)rows * g * nslices / kWave;
-        int split = waves < 4096 ? 2 : 1;
+        const int chunks = edges_per_row_hint > 0 ? edges_per_row_hint / u : 1 << 20;
+        int split = (waves < 2048 && chunks >= 6) ? 4 : (waves < 4096 && chunks >= 3) ? 2 : 1;
         if (const char* es = knob("GAT_EDGE_SPLIT")) {
             split = std::atoi(es);
             if (split != 2 && split != 4) split = 1;
