@@ -41,9 +41,7 @@ VARIANTS = {
     # (small test graphs take it by default)
     "split2": {"GAT_EDGE_SPLIT": "2"},
     "split1": {"GAT_EDGE_SPLIT": "1"},
-    "split2_u8_nosched": {"GAT_EDGE_SPLIT": "2", "GAT_EDGE_U": "8", "GAT_EDGE_SCHED": "0"},
     "split4": {"GAT_EDGE_SPLIT": "4"},
-    "split4_u8_nosched": {"GAT_EDGE_SPLIT": "4", "GAT_EDGE_U": "8", "GAT_EDGE_SCHED": "0"},
     # projection: k_project_x3 for 64 < fin <= 128 (WRES=0), k_project_wres for
     # every fin <= 128, the tiled fallback; plain stores instead of write-through
     "proj_wk": {"GAT_PROJ_WRES": "0"},
@@ -53,8 +51,6 @@ VARIANTS = {
     "plain_stores": {"GAT_STORE_WT": "0"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
-    "sliced8_v2": {"GAT_WH_SLICES": "8", "GAT_EDGE_V": "2"},
-    "sliced4_proj_pipe": {"GAT_WH_SLICES": "4", "GAT_PROJ_WK_MAX": "0"},
 }
 
 
