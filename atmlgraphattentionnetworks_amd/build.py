@@ -27,6 +27,11 @@ LIB = os.path.join(PKG, "libgat_amd.so")
 ARCH = os.environ.get("GAT_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
          "-munsafe-fp-atomics"]
+# GAT_AB_KERNELS=1: a tools-only build that also carries the measured-slower
+# kernels kept for A/B (the fp32-MFMA k_project_pipe2 behind GAT_PROJ_X3=0);
+# the product library never defines it.  Use --force when switching.
+if os.environ.get("GAT_AB_KERNELS"):
+    FLAGS.append("-DGAT_AB_KERNELS")
 
 
 def hipcc() -> str:
