@@ -3,7 +3,7 @@
 // in different table layouts?  Memory behaviour only: each lane accumulates a
 // product of what it loads, no softmax recompute.  Standalone HIP program.
 //
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/bwd_gather_probe.hip -o tools/bwd_gather_probe
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/bwd_gather_probe.hip -o tools/bwd_gather_probe
 //   tools/bwd_gather_probe [n] [deg]
 //
 // Layouts (per target i, HF = 64 columns of g plus (s_dst, lse, delta, 0) for 8 heads):
@@ -118,6 +118,307 @@ __global__ __launch_bounds__(256) void k_planes(const int* __restrict__ ptr,
     if (tot.x == 1234.5f) out[blockIdx.x] = tot.y;
 }
 
+// Bisection from the memory-only walk (k_row) toward the library's source
+// pass (gat_backward.hip k_bwd_sources, HF = 64, F = 8, concat), adding its
+// pieces cumulatively by LVL:
+//   1: the destination ids and the csc_eid stream loaded one chunk ahead
+//   2: + the per-edge arithmetic without dropout (z, exp2, dA head sum, dz,
+//      acc += A g, ds accumulation)
+//   3: + the dropout hash per (edge, head)
+//   4: + the per-row work: the source's Wh float4 and score, ds_dst, the dWh
+//      store and the per-wave parameter partials
+__device__ __forceinline__ unsigned pmix32(unsigned x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ float pdpp_b1(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+template <int G, int U, int LVL>
+__global__ __launch_bounds__(256) void k_pass(const int* __restrict__ ptr, const int* __restrict__ dst,
+                                              const int* __restrict__ eid, int n,
+                                              const float* __restrict__ T, int ld,
+                                              const float* __restrict__ Wh,
+                                              const float* __restrict__ dsd_all,
+                                              float* __restrict__ dwh, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63, c = lane & (G - 1), gbase = lane & ~(G - 1);
+    const int groups = gridDim.x * 256 / G;
+    const int gid = (blockIdx.x * 256 + threadIdx.x) / G;
+    const int h = c / 2;
+    const float slope = 0.2f, gs = 1.f, kl2e = 1.4426950408889634f;
+    const unsigned thresh = 2576980378u, seed = 12345u;  // p = 0.6
+    const f32x4 a1 = {0.01f * c, 0.02f, 0.03f, 0.04f}, a2 = {0.02f, 0.01f * c, 0.f, 0.01f};
+    f32x4 tot = {0.f, 0.f, 0.f, 0.f}, pa1 = tot, pa2 = tot, pdb = tot;
+    float pc = 0.f;
+    for (int j = gid; j < n; j += groups) {
+        f32x4 w4 = {0.1f, 0.2f, 0.3f, 0.4f};
+        float ssrc = 0.f;
+        if constexpr (LVL >= 4) {
+            w4 = *reinterpret_cast<const f32x4*>(Wh + (size_t)j * 64 + 4 * c);
+            ssrc = w4.x * a1.x + w4.y * a1.y + w4.z * a1.z + w4.w * a1.w;
+            ssrc += pdpp_b1(ssrc);
+        }
+        const int b0 = ptr[j], b1 = ptr[j + 1];
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        float dss = 0.f;
+        int iv = dst[max(min(b0 + c, b1 - 1), 0)];
+        int kv = eid[max(min(b0 + c, b1 - 1), 0)];
+        for (int b = b0; b < b1; b += U) {
+            const int nb = min(U, b1 - b);
+            const int in_ = dst[min(b + U + c, b1 - 1)];
+            const int kn = eid[min(b + U + c, b1 - 1)];
+            f32x4 gv[U], tv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = __shfl(iv, gbase + (u % G));
+                const float* tr = T + (size_t)i * ld;
+                gv[u] = *reinterpret_cast<const f32x4*>(tr + 4 * c);
+                tv[u] = *reinterpret_cast<const f32x4*>(tr + 64 + 4 * h);
+            }
+            if constexpr (LVL >= 2) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    float da = gv[u].x * w4.x + gv[u].y * w4.y + gv[u].z * w4.z + gv[u].w * w4.w;
+                    da += pdpp_b1(da);
+                    const float z = tv[u].x + ssrc;
+                    const float a = __builtin_amdgcn_exp2f((fmaxf(z, z * slope) - tv[u].y) * kl2e);
+                    float dm = 1.f;
+                    if constexpr (LVL >= 3) {
+                        const int kpos = __shfl(kv, gbase + (u % G));
+                        const unsigned long long idx = (unsigned long long)kpos * 8u + (unsigned)h;
+                        const unsigned x1 = pmix32((unsigned)idx ^ seed);
+                        const unsigned x2 = pmix32((unsigned)(idx >> 32) + 777u);
+                        dm = pmix32(x1 ^ x2) >= thresh ? 2.5f : 0.f;
+                    }
+                    const float de = a * (dm * da * gs - tv[u].z);
+                    const float dz = z > 0.f ? de : de * slope;
+                    const float w = u < nb ? a * dm : 0.f;
+                    acc += w * gv[u];
+                    dss += u < nb ? dz : 0.f;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u) acc += (b + u < b1 ? tv[u].x : 0.f) * gv[u];
+                dss += (float)kv;
+            }
+            iv = in_;
+            kv = kn;
+        }
+        if constexpr (LVL >= 4) {
+            const float dsd = dsd_all[(size_t)j * 8 + h];
+            const f32x4 d = acc * gs + dss * a1 + dsd * a2;
+            *reinterpret_cast<f32x4*>(dwh + (size_t)j * 64 + 4 * c) = d;
+            pa1 += dss * w4;
+            pa2 += dsd * w4;
+            pdb += d;
+            pc += dss;
+        } else {
+            tot += acc;
+            pc += dss;
+        }
+    }
+    tot += pa1 + pa2 + pdb;
+    if (tot.x == 1234.5f || pc == 1234.5f) out[blockIdx.x] = tot.y;  // keep the work
+}
+
+// LVL 4 with the gathers software-pipelined one chunk ahead: chunk k+1's
+// records are requested before chunk k is consumed (ids two chunks ahead), so
+// the per-edge arithmetic no longer sits between a chunk's arrival and the
+// next chunk's requests.
+template <int G, int U>
+__global__ __launch_bounds__(256) void k_pass_pipe(const int* __restrict__ ptr, const int* __restrict__ dst,
+                                                   const int* __restrict__ eid, int n,
+                                                   const float* __restrict__ T, int ld,
+                                                   const float* __restrict__ Wh,
+                                                   const float* __restrict__ dsd_all,
+                                                   float* __restrict__ dwh, float* __restrict__ out) {
+    const int lane = threadIdx.x & 63, c = lane & (G - 1), gbase = lane & ~(G - 1);
+    const int groups = gridDim.x * 256 / G;
+    const int gid = (blockIdx.x * 256 + threadIdx.x) / G;
+    const int h = c / 2;
+    const float slope = 0.2f, gs = 1.f, kl2e = 1.4426950408889634f;
+    const unsigned thresh = 2576980378u, seed = 12345u;
+    const f32x4 a1 = {0.01f * c, 0.02f, 0.03f, 0.04f}, a2 = {0.02f, 0.01f * c, 0.f, 0.01f};
+    f32x4 pa1 = {0.f, 0.f, 0.f, 0.f}, pa2 = pa1, pdb = pa1;
+    float pc = 0.f;
+    for (int j = gid; j < n; j += groups) {
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(Wh + (size_t)j * 64 + 4 * c);
+        float ssrc = w4.x * a1.x + w4.y * a1.y + w4.z * a1.z + w4.w * a1.w;
+        ssrc += pdpp_b1(ssrc);
+        const int b0 = ptr[j], b1 = ptr[j + 1];
+        if (b1 <= b0) continue;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        float dss = 0.f;
+        int iv = dst[min(b0 + c, b1 - 1)], kv = eid[min(b0 + c, b1 - 1)];
+        int iv1 = dst[min(b0 + U + c, b1 - 1)], kv1 = eid[min(b0 + U + c, b1 - 1)];
+        f32x4 gv[U], tv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = __shfl(iv, gbase + (u % G));
+            gv[u] = *reinterpret_cast<const f32x4*>(T + (size_t)i * ld + 4 * c);
+            tv[u] = *reinterpret_cast<const f32x4*>(T + (size_t)i * ld + 64 + 4 * h);
+        }
+        for (int b = b0; b < b1; b += U) {
+            const int nb = min(U, b1 - b);
+            const int iv2 = dst[min(b + 2 * U + c, b1 - 1)], kv2 = eid[min(b + 2 * U + c, b1 - 1)];
+            f32x4 gn[U], tn[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // next chunk's records (clamped: always valid)
+                const int i = __shfl(iv1, gbase + (u % G));
+                gn[u] = *reinterpret_cast<const f32x4*>(T + (size_t)i * ld + 4 * c);
+                tn[u] = *reinterpret_cast<const f32x4*>(T + (size_t)i * ld + 64 + 4 * h);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float da = gv[u].x * w4.x + gv[u].y * w4.y + gv[u].z * w4.z + gv[u].w * w4.w;
+                da += pdpp_b1(da);
+                const float z = tv[u].x + ssrc;
+                const float a = __builtin_amdgcn_exp2f((fmaxf(z, z * slope) - tv[u].y) * kl2e);
+                const int kpos = __shfl(kv, gbase + (u % G));
+                const unsigned long long idx = (unsigned long long)kpos * 8u + (unsigned)h;
+                const unsigned x1 = pmix32((unsigned)idx ^ seed);
+                const unsigned x2 = pmix32((unsigned)(idx >> 32) + 777u);
+                const float dm = pmix32(x1 ^ x2) >= thresh ? 2.5f : 0.f;
+                const float de = a * (dm * da * gs - tv[u].z);
+                const float dz = z > 0.f ? de : de * slope;
+                const float w = u < nb ? a * dm : 0.f;
+                acc += w * gv[u];
+                dss += u < nb ? dz : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                gv[u] = gn[u];
+                tv[u] = tn[u];
+            }
+            iv = iv1; kv = kv1; iv1 = iv2; kv1 = kv2;
+        }
+        const float dsd = dsd_all[(size_t)j * 8 + h];
+        const f32x4 d = acc * gs + dss * a1 + dsd * a2;
+        *reinterpret_cast<f32x4*>(dwh + (size_t)j * 64 + 4 * c) = d;
+        pa1 += dss * w4;
+        pa2 += dsd * w4;
+        pdb += d;
+        pc += dss;
+    }
+    const f32x4 tot = pa1 + pa2 + pdb;
+    if (tot.x == 1234.5f || pc == 1234.5f) out[blockIdx.x] = tot.y;
+}
+
+// LVL 4 with the per-(edge, head) scalar chain (record, z, exp2, hash, dz)
+// split between a head's two lanes (lane parity p takes edges 2v + p) and the
+// coefficient handed over by one DPP swap; V2: one lane per head, two g
+// float4s per lane (G = 8), so the scalar chain runs once per (edge, head)
+template <int G, int U, bool V2>
+__global__ __launch_bounds__(256) void k_pass_split(const int* __restrict__ ptr, const int* __restrict__ dst,
+                                                    const int* __restrict__ eid, int n,
+                                                    const float* __restrict__ T, int ld,
+                                                    const float* __restrict__ Wh,
+                                                    const float* __restrict__ dsd_all,
+                                                    float* __restrict__ dwh, float* __restrict__ out) {
+    constexpr int VV = V2 ? 2 : 1;
+    const int lane = threadIdx.x & 63, c = lane & (G - 1), gbase = lane & ~(G - 1);
+    const int groups = gridDim.x * 256 / G;
+    const int gid = (blockIdx.x * 256 + threadIdx.x) / G;
+    const int h = V2 ? c : c / 2;
+    const int par = c & 1;
+    const float slope = 0.2f, gs = 1.f, kl2e = 1.4426950408889634f;
+    const unsigned thresh = 2576980378u, seed = 12345u;
+    const f32x4 a1 = {0.01f * c, 0.02f, 0.03f, 0.04f}, a2 = {0.02f, 0.01f * c, 0.f, 0.01f};
+    f32x4 pa1 = {0.f, 0.f, 0.f, 0.f}, pa2 = pa1, pdb = pa1;
+    float pc = 0.f;
+    for (int j = gid; j < n; j += groups) {
+        f32x4 w4[VV];
+        float ssrc = 0.f;
+#pragma unroll
+        for (int q = 0; q < VV; ++q) {
+            w4[q] = *reinterpret_cast<const f32x4*>(Wh + (size_t)j * 64 + 4 * (VV * c + q));
+            ssrc += w4[q].x * a1.x + w4[q].y * a1.y + w4[q].z * a1.z + w4[q].w * a1.w;
+        }
+        if (!V2) ssrc += pdpp_b1(ssrc);
+        const int b0 = ptr[j], b1 = ptr[j + 1];
+        f32x4 acc[VV];
+#pragma unroll
+        for (int q = 0; q < VV; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float dss = 0.f;
+        int iv = dst[max(min(b0 + c, b1 - 1), 0)], kv = eid[max(min(b0 + c, b1 - 1), 0)];
+        int iv_b = V2 ? dst[max(min(b0 + G + c, b1 - 1), 0)] : 0;
+        int kv_b = V2 ? eid[max(min(b0 + G + c, b1 - 1), 0)] : 0;
+        for (int b = b0; b < b1; b += U) {
+            const int nb = min(U, b1 - b);
+            const int in_ = dst[min(b + U + c, b1 - 1)], kn = eid[min(b + U + c, b1 - 1)];
+            const int in_b = V2 ? dst[min(b + U + G + c, b1 - 1)] : 0;
+            const int kn_b = V2 ? eid[min(b + U + G + c, b1 - 1)] : 0;
+            f32x4 gv[U][VV];
+            f32x4 tv[V2 ? U : U / 2];
+            int io[V2 ? U : U / 2], ko[V2 ? U : U / 2];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int src = u < G ? iv : iv_b;
+                const int i = __shfl(src, gbase + (u % G));
+                const int ksrc = u < G ? kv : kv_b;
+                const int kk = __shfl(ksrc, gbase + (u % G));
+#pragma unroll
+                for (int q = 0; q < VV; ++q)
+                    gv[u][q] = *reinterpret_cast<const f32x4*>(T + (size_t)i * ld + 4 * (VV * c + q));
+                if (V2) { io[u] = i; ko[u] = kk; }
+                else if (u % 2 == 0) { io[u / 2] = i; ko[u / 2] = kk; }
+                else if (par) { io[u / 2] = i; ko[u / 2] = kk; }
+            }
+#pragma unroll
+            for (int v = 0; v < (V2 ? U : U / 2); ++v)
+                tv[v] = *reinterpret_cast<const f32x4*>(T + (size_t)io[v] * ld + 64 + 4 * h);
+            float dd[V2 ? U : U / 2];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float d = 0.f;
+#pragma unroll
+                for (int q = 0; q < VV; ++q)
+                    d += gv[u][q].x * w4[q].x + gv[u][q].y * w4[q].y + gv[u][q].z * w4[q].z + gv[u][q].w * w4[q].w;
+                if (!V2) d += pdpp_b1(d);
+                if (V2) dd[u] = d;
+                else if (u % 2 == 0) dd[u / 2] = d;
+                else if (par) dd[u / 2] = d;
+            }
+#pragma unroll
+            for (int v = 0; v < (V2 ? U : U / 2); ++v) {
+                const int uo = V2 ? v : 2 * v + par;
+                const float z = tv[v].x + ssrc;
+                const float a = __builtin_amdgcn_exp2f((fmaxf(z, z * slope) - tv[v].y) * kl2e);
+                const unsigned long long idx = (unsigned long long)ko[v] * 8u + (unsigned)h;
+                const unsigned x1 = pmix32((unsigned)idx ^ seed);
+                const unsigned x2 = pmix32((unsigned)(idx >> 32) + 777u);
+                const float dm = pmix32(x1 ^ x2) >= thresh ? 2.5f : 0.f;
+                const float de = a * (dm * dd[v] * gs - tv[v].z);
+                const float dz = z > 0.f ? de : de * slope;
+                const float wo = uo < nb ? a * dm : 0.f;
+                dss += uo < nb ? dz : 0.f;
+                if (V2) {
+#pragma unroll
+                    for (int q = 0; q < VV; ++q) acc[q] += wo * gv[v][q];
+                } else {
+                    const float wp = pdpp_b1(wo);
+                    acc[0] += (par ? wp : wo) * gv[2 * v][0];
+                    acc[0] += (par ? wo : wp) * gv[2 * v + 1][0];
+                }
+            }
+            iv = in_; kv = kn; iv_b = in_b; kv_b = kn_b;
+        }
+        if (!V2) dss += pdpp_b1(dss);
+        const float dsd = dsd_all[(size_t)j * 8 + h];
+#pragma unroll
+        for (int q = 0; q < VV; ++q) {
+            const f32x4 d = acc[q] * gs + dss * a1 + dsd * a2;
+            *reinterpret_cast<f32x4*>(dwh + (size_t)j * 64 + 4 * (VV * c + q)) = d;
+            pa1 += dss * w4[q];
+            pa2 += dsd * w4[q];
+            pdb += d;
+        }
+        pc += dss;
+    }
+    const f32x4 tot = pa1 + pa2 + pdb;
+    if (tot.x == 1234.5f || pc == 1234.5f) out[blockIdx.x] = tot.y;
+}
+
 static float time_it(hipStream_t st, int reps, auto&& f) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -173,6 +474,35 @@ int main(int argc, char** argv) {
         rep(nm, time_it(st, reps, [&] { k_planes<2, 16, 16, 12, 64><<<(waves / 4 / 2) * 2, 256, 0, st>>>(ptr, dst, n, T, out); }), 512);
         snprintf(nm, sizeof nm, "planes1_384B_U16_w%d", waves);
         rep(nm, time_it(st, reps, [&] { k_planes<1, 32, 16, 24, 96><<<waves / 4, 256, 0, st>>>(ptr, dst, n, T, out); }), 384);
+    }
+    {   // bisection toward the library's source pass (k_pass LVL 1-4), 58k waves as the pass
+        int* eid;
+        float *Wh, *dsd, *dwh;
+        CK(hipMalloc(&eid, nnz * 4));
+        CK(hipMalloc(&Wh, (size_t)n * 64 * 4));
+        CK(hipMalloc(&dsd, (size_t)n * 8 * 4));
+        CK(hipMalloc(&dwh, (size_t)n * 64 * 4));
+        CK(hipMemsetAsync(Wh, 0, (size_t)n * 64 * 4, st));
+        CK(hipMemsetAsync(dsd, 0, (size_t)n * 8 * 4, st));
+        k_make_csc<<<4096, 256, 0, st>>>(n, deg, ptr, eid);  // a permutation-like id stream
+        CK(hipStreamSynchronize(st));
+        const int grid = ((n * 16 + 63) / 64 + 3) / 4;
+        rep("pass_L1_ids_eid_prefetch", time_it(st, reps, [&] { k_pass<16, 16, 1><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_L2_math_nodrop", time_it(st, reps, [&] { k_pass<16, 16, 2><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_L3_math_drop", time_it(st, reps, [&] { k_pass<16, 16, 3><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_L4_full", time_it(st, reps, [&] { k_pass<16, 16, 4><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_L4_full_U8", time_it(st, reps, [&] { k_pass<16, 8, 4><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_L4_full_U4", time_it(st, reps, [&] { k_pass<16, 4, 4><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_pipe_U8", time_it(st, reps, [&] { k_pass_pipe<16, 8><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_pipe_U4", time_it(st, reps, [&] { k_pass_pipe<16, 4><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_pipe_U16", time_it(st, reps, [&] { k_pass_pipe<16, 16><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_split_pair_U16", time_it(st, reps, [&] { k_pass_split<16, 16, false><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_split_pair_U8", time_it(st, reps, [&] { k_pass_split<16, 8, false><<<grid, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        const int grid8 = ((n * 8 + 63) / 64 + 3) / 4;
+        rep("pass_split_v2_U8", time_it(st, reps, [&] { k_pass_split<8, 8, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_split_v2_U16", time_it(st, reps, [&] { k_pass_split<8, 16, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_split_v2_U4", time_it(st, reps, [&] { k_pass_split<8, 4, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("row384_U16_pass_grid", time_it(st, reps, [&] { k_row<16, 16><<<grid, 256, 0, st>>>(ptr, dst, n, T, 96, out); }), 384);
     }
     // the forward's table for comparison: 2 planes of 128-B rows (32 floats)
     rep("fwd_planes2_128B_U16_w32768", time_it(st, reps, [&] { k_planes<2, 8, 16, 8, 32><<<8192, 256, 0, st>>>(ptr, dst, n, T, out); }), 256, true);
