@@ -19,6 +19,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                         \
@@ -308,7 +309,9 @@ __global__ __launch_bounds__(256) void k_pass_pipe(const int* __restrict__ ptr, 
 // split between a head's two lanes (lane parity p takes edges 2v + p) and the
 // coefficient handed over by one DPP swap; V2: one lane per head, two g
 // float4s per lane (G = 8), so the scalar chain runs once per (edge, head)
-template <int G, int U, bool V2>
+// RT: the dropout threshold, seeds and scale come from memory (as the
+// library's runtime DropArgs) instead of being literals
+template <int G, int U, bool V2, bool RT = false>
 __global__ __launch_bounds__(256) void k_pass_split(const int* __restrict__ ptr, const int* __restrict__ dst,
                                                     const int* __restrict__ eid, int n,
                                                     const float* __restrict__ T, int ld,
@@ -322,7 +325,10 @@ __global__ __launch_bounds__(256) void k_pass_split(const int* __restrict__ ptr,
     const int h = V2 ? c : c / 2;
     const int par = c & 1;
     const float slope = 0.2f, gs = 1.f, kl2e = 1.4426950408889634f;
-    const unsigned thresh = 2576980378u, seed = 12345u;
+    const unsigned thresh = RT ? __float_as_uint(dsd_all[100]) : 2576980378u;
+    const unsigned seed = RT ? __float_as_uint(dsd_all[101]) : 12345u;
+    const unsigned seedhi = RT ? __float_as_uint(dsd_all[102]) : 777u;
+    const float dscale = RT ? dsd_all[103] : 2.5f;
     const f32x4 a1 = {0.01f * c, 0.02f, 0.03f, 0.04f}, a2 = {0.02f, 0.01f * c, 0.f, 0.01f};
     f32x4 pa1 = {0.f, 0.f, 0.f, 0.f}, pa2 = pa1, pdb = pa1;
     float pc = 0.f;
@@ -386,8 +392,8 @@ __global__ __launch_bounds__(256) void k_pass_split(const int* __restrict__ ptr,
                 const float a = __builtin_amdgcn_exp2f((fmaxf(z, z * slope) - tv[v].y) * kl2e);
                 const unsigned long long idx = (unsigned long long)ko[v] * 8u + (unsigned)h;
                 const unsigned x1 = pmix32((unsigned)idx ^ seed);
-                const unsigned x2 = pmix32((unsigned)(idx >> 32) + 777u);
-                const float dm = pmix32(x1 ^ x2) >= thresh ? 2.5f : 0.f;
+                const unsigned x2 = pmix32((unsigned)(idx >> 32) + seedhi);
+                const float dm = pmix32(x1 ^ x2) >= thresh ? dscale : 0.f;
                 const float de = a * (dm * dd[v] * gs - tv[v].z);
                 const float dz = z > 0.f ? de : de * slope;
                 const float wo = uo < nb ? a * dm : 0.f;
@@ -484,6 +490,12 @@ int main(int argc, char** argv) {
         CK(hipMalloc(&dwh, (size_t)n * 64 * 4));
         CK(hipMemsetAsync(Wh, 0, (size_t)n * 64 * 4, st));
         CK(hipMemsetAsync(dsd, 0, (size_t)n * 8 * 4, st));
+        {   // the RT variant's dropout parameters (p = 0.6) at dsd[100..103]
+            unsigned prm[4] = {2576980378u, 12345u, 777u, 0u};
+            const float sc = 2.5f;
+            memcpy(&prm[3], &sc, 4);
+            CK(hipMemcpyAsync(dsd + 100, prm, 16, hipMemcpyHostToDevice, st));
+        }
         k_make_csc<<<4096, 256, 0, st>>>(n, deg, ptr, eid);  // a permutation-like id stream
         CK(hipStreamSynchronize(st));
         const int grid = ((n * 16 + 63) / 64 + 3) / 4;
@@ -501,6 +513,7 @@ int main(int argc, char** argv) {
         const int grid8 = ((n * 8 + 63) / 64 + 3) / 4;
         rep("pass_split_v2_U8", time_it(st, reps, [&] { k_pass_split<8, 8, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
         rep("pass_split_v2_U16", time_it(st, reps, [&] { k_pass_split<8, 16, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("pass_split_v2_U8_rtdrop", time_it(st, reps, [&] { k_pass_split<8, 8, true, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
         rep("pass_split_v2_U4", time_it(st, reps, [&] { k_pass_split<8, 4, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
         rep("row384_U16_pass_grid", time_it(st, reps, [&] { k_row<16, 16><<<grid, 256, 0, st>>>(ptr, dst, n, T, 96, out); }), 384);
     }
