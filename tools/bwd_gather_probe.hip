@@ -52,6 +52,23 @@ __global__ void k_make_csc(int n, int deg, int* __restrict__ ptr, int* __restric
     }
 }
 
+// independent random ascending targets per source (gaps uniform in
+// [0, 2n/deg)): the uniform graph's sorted CSC rows, without the stratified
+// walk's alignment across sources
+__global__ void k_make_csc_random(int n, int deg, int* __restrict__ dst) {
+    const long j = blockIdx.x * 256L + threadIdx.x;
+    if (j >= n) return;
+    unsigned st = (unsigned)j * 2654435761u + 0x9e3779b9u;
+    double t = 0.0;
+    const double span = 2.0 * n / deg;
+    for (int k = 0; k < deg; ++k) {
+        st ^= st << 13; st ^= st >> 17; st ^= st << 5;
+        t += (st & 0xFFFFFF) / 16777216.0 * span;
+        const int v = (int)t;
+        dst[j * (long)deg + k] = v < n ? v : n - 1;
+    }
+}
+
 template <int G, int U>
 __global__ __launch_bounds__(256) void k_row(const int* __restrict__ ptr, const int* __restrict__ dst,
                                              int n, const float* __restrict__ T, int ld,
@@ -516,6 +533,24 @@ int main(int argc, char** argv) {
         rep("pass_split_v2_U8_rtdrop", time_it(st, reps, [&] { k_pass_split<8, 8, true, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
         rep("pass_split_v2_U4", time_it(st, reps, [&] { k_pass_split<8, 4, true><<<grid8, 256, 0, st>>>(ptr, dst, eid, n, T, 96, Wh, dsd, dwh, out); }), 384);
         rep("row384_U16_pass_grid", time_it(st, reps, [&] { k_row<16, 16><<<grid, 256, 0, st>>>(ptr, dst, n, T, 96, out); }), 384);
+    }
+    {   // the same walk and full pass over a random (uniform-graph-like) CSC
+        int* eid2;
+        float *Wh, *dsd, *dwh;
+        CK(hipMalloc(&eid2, nnz * 4));
+        CK(hipMalloc(&Wh, (size_t)n * 64 * 4));
+        CK(hipMalloc(&dsd, (size_t)n * 8 * 4));
+        CK(hipMalloc(&dwh, (size_t)n * 64 * 4));
+        CK(hipMemsetAsync(Wh, 0, (size_t)n * 64 * 4, st));
+        CK(hipMemsetAsync(dsd, 0, (size_t)n * 8 * 4, st));
+        k_make_csc_random<<<(n + 255) / 256, 256, 0, st>>>(n, deg, dst);
+        k_make_csc<<<4096, 256, 0, st>>>(n, deg, ptr, eid2);
+        CK(hipStreamSynchronize(st));
+        const int grid = ((n * 16 + 63) / 64 + 3) / 4;
+        rep("random_row384_U16_pass_grid", time_it(st, reps, [&] { k_row<16, 16><<<grid, 256, 0, st>>>(ptr, dst, n, T, 96, out); }), 384);
+        rep("random_pass_L4_full", time_it(st, reps, [&] { k_pass<16, 16, 4><<<grid, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        const int grid8 = ((n * 8 + 63) / 64 + 3) / 4;
+        rep("random_pass_split_v2_U8_rtdrop", time_it(st, reps, [&] { k_pass_split<8, 8, true, true><<<grid8, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); }), 384);
     }
     // the forward's table for comparison: 2 planes of 128-B rows (32 floats)
     rep("fwd_planes2_128B_U16_w32768", time_it(st, reps, [&] { k_planes<2, 8, 16, 8, 32><<<8192, 256, 0, st>>>(ptr, dst, n, T, out); }), 256, true);
