@@ -69,6 +69,15 @@ __global__ void k_make_csc_random(int n, int deg, int* __restrict__ dst) {
     }
 }
 
+// fill a buffer with hashed values in [-1, 1) (non-zero table contents)
+__global__ void k_fill_random(float* __restrict__ p, long count, unsigned salt) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < count; i += (long)gridDim.x * 256) {
+        unsigned h = (unsigned)i * 2654435761u ^ salt;
+        h ^= h >> 15; h *= 0x2c1b3c6du; h ^= h >> 12;
+        p[i] = (h & 0xFFFFFF) / 8388608.f - 1.f;
+    }
+}
+
 template <int G, int U>
 __global__ __launch_bounds__(256) void k_row(const int* __restrict__ ptr, const int* __restrict__ dst,
                                              int n, const float* __restrict__ T, int ld,
@@ -551,6 +560,20 @@ int main(int argc, char** argv) {
         rep("random_pass_L4_full", time_it(st, reps, [&] { k_pass<16, 16, 4><<<grid, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); }), 384);
         const int grid8 = ((n * 8 + 63) / 64 + 3) / 4;
         rep("random_pass_split_v2_U8_rtdrop", time_it(st, reps, [&] { k_pass_split<8, 8, true, true><<<grid8, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        // non-zero table, Wh and ds_dst values (the dropout parameters at dsd[100..103] rewritten)
+        k_fill_random<<<4096, 256, 0, st>>>(T, (long)n * 96, 11u);
+        k_fill_random<<<4096, 256, 0, st>>>(Wh, (long)n * 64, 22u);
+        k_fill_random<<<4096, 256, 0, st>>>(dsd, (long)n * 8, 33u);
+        {
+            unsigned prm[4] = {2576980378u, 12345u, 777u, 0u};
+            const float sc = 2.5f;
+            memcpy(&prm[3], &sc, 4);
+            CK(hipMemcpyAsync(dsd + 100, prm, 16, hipMemcpyHostToDevice, st));
+        }
+        CK(hipStreamSynchronize(st));
+        rep("random_values_row384_U16", time_it(st, reps, [&] { k_row<16, 16><<<grid, 256, 0, st>>>(ptr, dst, n, T, 96, out); }), 384);
+        rep("random_values_pass_L4_full", time_it(st, reps, [&] { k_pass<16, 16, 4><<<grid, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("random_values_pass_split_v2_U8_rtdrop", time_it(st, reps, [&] { k_pass_split<8, 8, true, true><<<grid8, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); }), 384);
     }
     // the forward's table for comparison: 2 planes of 128-B rows (32 floats)
     rep("fwd_planes2_128B_U16_w32768", time_it(st, reps, [&] { k_planes<2, 8, 16, 8, 32><<<8192, 256, 0, st>>>(ptr, dst, n, T, out); }), 256, true);
