@@ -574,6 +574,16 @@ int main(int argc, char** argv) {
         rep("random_values_row384_U16", time_it(st, reps, [&] { k_row<16, 16><<<grid, 256, 0, st>>>(ptr, dst, n, T, 96, out); }), 384);
         rep("random_values_pass_L4_full", time_it(st, reps, [&] { k_pass<16, 16, 4><<<grid, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); }), 384);
         rep("random_values_pass_split_v2_U8_rtdrop", time_it(st, reps, [&] { k_pass_split<8, 8, true, true><<<grid8, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        // the table rewritten right before each pass (as k_bwd_table does in a training step):
+        // (fill + pass) - fill
+        {
+            const float fill = time_it(st, reps, [&] { k_fill_random<<<4096, 256, 0, st>>>(T, (long)n * 96, 11u); });
+            const float a = time_it(st, reps, [&] { k_fill_random<<<4096, 256, 0, st>>>(T, (long)n * 96, 11u); k_pass<16, 16, 4><<<grid, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); });
+            const float b = time_it(st, reps, [&] { k_fill_random<<<4096, 256, 0, st>>>(T, (long)n * 96, 11u); k_pass_split<8, 8, true, true><<<grid8, 256, 0, st>>>(ptr, dst, eid2, n, T, 96, Wh, dsd, dwh, out); });
+            rep("fresh_table_fill_only", fill, 384);
+            rep("fresh_table_pass_L4_full", a - fill, 384);
+            rep("fresh_table_pass_split_v2_U8_rtdrop", b - fill, 384);
+        }
     }
     // the forward's table for comparison: 2 planes of 128-B rows (32 floats)
     rep("fwd_planes2_128B_U16_w32768", time_it(st, reps, [&] { k_planes<2, 8, 16, 8, 32><<<8192, 256, 0, st>>>(ptr, dst, n, T, out); }), 256, true);
