@@ -78,6 +78,22 @@ __global__ void k_fill_random(float* __restrict__ p, long count, unsigned salt) 
     }
 }
 
+// random ascending targets per source with a per-source out-degree (ptr given)
+__global__ void k_make_csc_var(int n, const int* __restrict__ ptr, int* __restrict__ dst) {
+    const long j = blockIdx.x * 256L + threadIdx.x;
+    if (j >= n) return;
+    const int b0 = ptr[j], deg = ptr[j + 1] - b0;
+    unsigned st = (unsigned)j * 2654435761u + 0x9e3779b9u;
+    double t = 0.0;
+    const double span = 2.0 * n / (deg > 0 ? deg : 1);
+    for (int k = 0; k < deg; ++k) {
+        st ^= st << 13; st ^= st >> 17; st ^= st << 5;
+        t += (st & 0xFFFFFF) / 16777216.0 * span;
+        const int v = (int)t;
+        dst[b0 + k] = v < n ? v : n - 1;
+    }
+}
+
 template <int G, int U>
 __global__ __launch_bounds__(256) void k_row(const int* __restrict__ ptr, const int* __restrict__ dst,
                                              int n, const float* __restrict__ T, int ld,
@@ -584,6 +600,40 @@ int main(int argc, char** argv) {
             rep("fresh_table_pass_L4_full", a - fill, 384);
             rep("fresh_table_pass_split_v2_U8_rtdrop", b - fill, 384);
         }
+    }
+    {   // out-degrees that vary per source (deg +- 22, about the binomial spread of a
+        // uniform graph's), random ascending targets
+        std::vector<int> hp(n + 1, 0);
+        unsigned st2 = 12345u;
+        for (int j = 0; j < n; ++j) {
+            st2 = st2 * 1664525u + 1013904223u;
+            hp[j + 1] = hp[j] + deg - 22 + (int)((st2 >> 8) % 45);
+        }
+        const long nnz2 = hp[n];
+        int *ptr2, *dst2, *eid3;
+        float *Wh, *dsd, *dwh;
+        CK(hipMalloc(&ptr2, (n + 1) * 4));
+        CK(hipMalloc(&dst2, nnz2 * 4));
+        CK(hipMalloc(&eid3, nnz2 * 4));
+        CK(hipMalloc(&Wh, (size_t)n * 64 * 4));
+        CK(hipMalloc(&dsd, (size_t)n * 8 * 4));
+        CK(hipMalloc(&dwh, (size_t)n * 64 * 4));
+        CK(hipMemcpy(ptr2, hp.data(), (n + 1) * 4, hipMemcpyHostToDevice));
+        k_make_csc_var<<<(n + 255) / 256, 256, 0, st>>>(n, ptr2, dst2);
+        CK(hipMemcpyAsync(eid3, dst2, nnz2 * 4, hipMemcpyDeviceToDevice, st));
+        k_fill_random<<<4096, 256, 0, st>>>(Wh, (long)n * 64, 22u);
+        k_fill_random<<<4096, 256, 0, st>>>(dsd, (long)n * 8, 33u);
+        {
+            unsigned prm[4] = {2576980378u, 12345u, 777u, 0u};
+            const float sc = 2.5f;
+            memcpy(&prm[3], &sc, 4);
+            CK(hipMemcpyAsync(dsd + 100, prm, 16, hipMemcpyHostToDevice, st));
+        }
+        CK(hipStreamSynchronize(st));
+        const int grid = ((n * 16 + 63) / 64 + 3) / 4;
+        const int grid8 = ((n * 8 + 63) / 64 + 3) / 4;
+        rep("vardeg_pass_L4_full", time_it(st, reps, [&] { k_pass<16, 16, 4><<<grid, 256, 0, st>>>(ptr2, dst2, eid3, n, T, 96, Wh, dsd, dwh, out); }), 384);
+        rep("vardeg_pass_split_v2_U8_rtdrop", time_it(st, reps, [&] { k_pass_split<8, 8, true, true><<<grid8, 256, 0, st>>>(ptr2, dst2, eid3, n, T, 96, Wh, dsd, dwh, out); }), 384);
     }
     // the forward's table for comparison: 2 planes of 128-B rows (32 floats)
     rep("fwd_planes2_128B_U16_w32768", time_it(st, reps, [&] { k_planes<2, 8, 16, 8, 32><<<8192, 256, 0, st>>>(ptr, dst, n, T, out); }), 256, true);
