@@ -169,3 +169,21 @@ def test_header_compiles_and_links_from_plain_c(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     assert r.stdout.startswith("c-abi ok 72 96")
+
+
+def test_every_library_knob_is_registered():
+    """Every GAT_* knob the HIP sources read must be in the snapshot registry
+    (gat_abi.hip kKnobNames): knob() returns null for an unregistered name, so
+    an A/B through such a knob silently runs the default path in both arms."""
+    import glob
+    import re
+    csrc = os.path.join(ROOT, "atmlgraphattentionnetworks_amd", "csrc")
+    used = set()
+    for path in glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")):
+        text = open(path).read()
+        used |= set(re.findall(r'(?:knob|kernel_choice)\("(GAT_[A-Z0-9_]+)"', text))
+    abi = open(os.path.join(csrc, "gat_abi.hip")).read()
+    reg = abi[abi.index("kKnobNames[]"):abi.index("};", abi.index("kKnobNames[]"))]
+    registered = set(re.findall(r'"(GAT_[A-Z0-9_]+)"', reg))
+    assert used, "no knob uses found"
+    assert used <= registered, f"unregistered knobs: {sorted(used - registered)}"
