@@ -492,6 +492,15 @@ __device__ __forceinline__ void split3_pair(f32x2 v, bf16x2& p1, bf16x2& p2, bf1
     p3 = __builtin_convertvector(r2, bf16x2);
 }
 
+// acc + cor of the split form.  For an infinite x element the split gives
+// x1 = x and x2 = x - x1 = NaN, so the correction sum is NaN while acc (x1.w1)
+// already holds what the reference's fp32 sum gives (+-Inf, or NaN for Inf*0
+// and Inf - Inf, which acc reproduces term for term): keep acc when it is
+// infinite.  Finite x: acc + cor, unchanged.
+__device__ __forceinline__ float split_sum(float a, float c) {
+    return __builtin_isinf(a) ? a : a + c;
+}
+
 __device__ __forceinline__ void split3_x8(f32x4 a, f32x4 b, bf16x8& h1, bf16x8& h2, bf16x8& h3) {
     bf16x2 p1[4], p2[4], p3[4];
     split3_pair(f32x2{a.x, a.y}, p1[0], p2[0], p3[0]);
@@ -665,7 +674,9 @@ __global__ __launch_bounds__(256) void k_project_x3(
 #pragma unroll
     for (int g = 0; g < RG; ++g)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[g][t] += cor[g][t];
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[g][t][i] = split_sum(acc[g][t][i], cor[g][t][i]);
 
     const int hfp = round_up4(HF);
     const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
@@ -887,7 +898,7 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
             float p1[4], p2[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float v = acc[t][i] + cor[t][i] + bb[t];  // Linear bias (GAT.py:43)
+                const float v = split_sum(acc[t][i], cor[t][i]) + bb[t];  // + bias (GAT.py:43)
                 Os[(kq * 4 + i) * OS + cc] = cc < HF ? v : 0.f;
                 p1[i] = group_sum16(v * w1[t], F);
                 p2[i] = group_sum16(v * w2[t], F);

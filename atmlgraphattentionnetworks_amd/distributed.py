@@ -818,7 +818,9 @@ def bench_distributed(args, metric: str):
     os.dup2(saved_stdout, 1)
     os.close(saved_stdout)
     if res is not None:
-        print(json.dumps(res), flush=True)
+        from .benchline import compact_dist, write_detail
+        path = write_detail(res, getattr(args, "detail_out", None))
+        print(json.dumps(compact_dist(res, path)), flush=True)
 
 
 def _free_port() -> int:

@@ -234,9 +234,17 @@ class _CSRCache:
             return hit[1]
         csr = build_csr(edge_index, num_nodes, device)
         self._entries[key] = (weakref.ref(edge_index), csr)
+        # the entry goes when its edge_index does: the cache must not keep a
+        # graph the caller dropped (a CSR can be GBs) alive until LRU eviction
+        weakref.finalize(edge_index, self._drop_dead, key)
         while len(self._entries) > self.capacity:
             self._entries.popitem(last=False)
         return csr
+
+    def _drop_dead(self, key) -> None:
+        hit = self._entries.get(key)
+        if hit is not None and hit[0]() is None:
+            del self._entries[key]
 
     def clear(self) -> None:
         self._entries.clear()

@@ -311,7 +311,7 @@ class ForwardPlan:
     projects into the table the previous forward did NOT read."""
 
     __slots__ = ("n", "fin", "heads", "f", "hf", "hfp", "concat", "slope", "slices", "split",
-                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched", "csr", "bound",
+                 "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched", "_csr", "bound",
                  "bufs", "cur")
 
     def __init__(self, x: torch.Tensor, csr: CSRGraph, heads: int, f: int, concat: bool,
@@ -344,16 +344,24 @@ class ForwardPlan:
         if (not self.split and fused_score_ok(heads, f, negative_slope)
                 and isinstance(csr, CSRGraph)):
             self.sched = sched_csr(csr)
-        self.csr = csr
+        # weak: a plan the layer caches must not keep a graph the caller dropped
+        # alive (CSRGraph is a tuple, so the weak reference is to its rowptr)
+        self._csr = weakref.ref(csr.rowptr)
         self.bound = None  # (pp, bias, lib, project call, edge call) for run()
 
+    def built_for(self, csr) -> bool:
+        """This plan was built for `csr` (and that graph is still alive)."""
+        return self._csr() is csr.rowptr
+
     def run(self, lib, x: torch.Tensor, pp: PackedParams, bias: torch.Tensor,
-            out: torch.Tensor) -> torch.Tensor:
+            out: torch.Tensor, csr: CSRGraph) -> torch.Tensor:
         """project() + edge() for a plan the layer caches between forwards: the
         argument lists (everything but x, out and the stream) are bound once
         per (parameters, bias), so a forward costs two C-ABI calls and little
         Python.  Safe to reuse the workspace: calls on one stream run in order,
         and the layer keys its cached plans by stream."""
+        if not self.built_for(csr):
+            raise ValueError("ForwardPlan.run: called with a graph the plan was not built for")
         if len(self.bufs) > 1:  # alternate workspaces (pingpong)
             self.cur ^= 1
             self.p_wh, self.p_ss, self.p_sd = self.bufs[self.cur]
@@ -362,8 +370,8 @@ class ForwardPlan:
                 self.split or self.slices == 1 and b[5]:
             if self.split or self.sched is None:
                 self.project(lib, x, pp)
-                return self.edge(lib, self.csr, pp, bias, out)
-            b = self.bound = self._bind(lib, pp, bias)
+                return self.edge(lib, csr, pp, bias, out)
+            b = self.bound = self._bind(lib, pp, bias, csr)
         stream = torch._C._cuda_getCurrentRawStream(self.dev)
         # projection + edge kernel in one C-ABI call (gat_layer_forward)
         rc = b[3](x.data_ptr(), *b[4][self.cur], out.data_ptr(), self.khint, stream)
@@ -373,15 +381,15 @@ class ForwardPlan:
                 # row-major table (project() decides)
                 self.bound = None
                 self.project(lib, x, pp)
-                return self.edge(lib, self.csr, pp, bias, out)
+                return self.edge(lib, csr, pp, bias, out)
             _lib.check(rc, "gat_layer_forward")
         return out
 
-    def _bind(self, lib, pp: PackedParams, bias: torch.Tensor):
+    def _bind(self, lib, pp: PackedParams, bias: torch.Tensor, csr: CSRGraph):
         n, fin, heads, f, sc = self.n, self.fin, self.heads, self.f, self.sched
         pw = (pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(), pp.c_src.data_ptr(),
               pp.a_dst.data_ptr(), pp.c_dst.data_ptr())
-        p_order = 0 if self.csr.order is None else self.csr.order.data_ptr()
+        p_order = 0 if csr.order is None else csr.order.data_ptr()
         fargs = []
         for p_wh, p_ss, p_sd in self.bufs:  # one argument list per workspace
             fargs.append((n, fin, *pw, heads, f, self.slices, p_wh, p_ss, p_sd, sc.b.data_ptr(),
@@ -516,6 +524,10 @@ def _check_x(x: torch.Tensor, in_channels: int) -> torch.Tensor:
     return x.contiguous()
 
 
+# layer -> OrderedDict of its cached eval ForwardPlans (GraphAttentionLayer._eval_forward)
+_eval_plans: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
 class GraphAttentionLayer(torch.nn.Module):
     """MI355X-native drop-in for the reference ``GraphAttentionLayer``
     (``GAT.py:6``): ``__init__(input_channels, output_channels, num_heads=1,
@@ -648,21 +660,26 @@ class GraphAttentionLayer(torch.nn.Module):
         and bound argument lists are reused, so a forward allocates only its
         output.  Small graphs (the CIFAR batch: ~15 us of GPU work) are
         host-bound, and this path is most of their host cost."""
-        plans = self.__dict__.get("_eval_plans")
+        # The plans live in a side table keyed weakly by the layer, not in the
+        # module's __dict__: a deepcopy or pickle of the layer must not carry
+        # workspaces, raw device pointers or ctypes function pointers along.
+        plans = _eval_plans.get(self)
         if plans is None:
-            plans = self.__dict__["_eval_plans"] = collections.OrderedDict()
+            plans = _eval_plans[self] = collections.OrderedDict()
+        for k in [k for k, p in plans.items() if p._csr() is None]:  # graphs since freed
+            del plans[k]
         dev = x.device.index
         key = (id(csr), x.shape[0], x.shape[1], slope, dev,
                torch._C._cuda_getCurrentRawStream(dev), tuning.generation)
         plan = plans.get(key)
-        if plan is None or plan.csr is not csr:
+        if plan is None or not plan.built_for(csr):
             plan = plans[key] = ForwardPlan(x, csr, self.num_heads, self.output_channels,
                                             self.concat, slope, pingpong=True)
             while len(plans) > 4:
                 plans.popitem(last=False)
         out = torch.empty(plan.n, plan.hf if self.concat else self.output_channels,
                           dtype=torch.float32, device=x.device)
-        return plan.run(_lib.load(), x, self.packed(), self.bias.detach(), out)
+        return plan.run(_lib.load(), x, self.packed(), self.bias.detach(), out, csr)
 
     def extra_repr(self) -> str:
         return (f"{self.input_channels}, {self.output_channels}, num_heads={self.num_heads}, "

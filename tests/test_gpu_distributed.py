@@ -180,7 +180,16 @@ def test_reddit_scale_partitioned_p8():
     torch.testing.assert_close(full[rows].cpu(), ref[rows.cpu()], atol=ATOL, rtol=RTOL)
 
 
-def test_bench_two_ranks_shared_gpu():
+def _one_line(stdout: str, budget: int = 8000):
+    """Exactly one non-empty stdout line, under the driver's parse budget."""
+    import json
+    lines = [ln for ln in stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, stdout[-2000:]
+    assert len(lines[0].encode()) < budget, len(lines[0])
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_shared_gpu(tmp_path):
     """bench.py --gpus 2 end to end with 2 torchrun ranks on cuda:0
     (GAT_BENCH_SHARE_GPU0; the all-gather staged through gloo because RCCL
     refuses two ranks on one device): the chunked shared-graph step, the
@@ -198,13 +207,15 @@ def test_bench_two_ranks_shared_gpu():
     env = dict(os.environ, GAT_BENCH_SHARE_GPU0="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-           "--dist-workloads", "ppi,arxiv", "--steps", "6", "--warmup", "2"]
+           "--dist-workloads", "ppi,arxiv", "--steps", "6", "--warmup", "2",
+           "--detail-out", str(tmp_path / "detail.json")]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
-    assert len(lines) == 1, r.stdout[-2000:]
-    d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
+    line = _one_line(r.stdout)
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
+    assert line["headline"]["check_max_abs_diff"] is not None
+    d = json.load(open(tmp_path / "detail.json"))  # the full detail
+    assert d["value"] == line["value"] or abs(d["value"] / line["value"] - 1) < 1e-3
     assert d["steps"] == 6 and d["unit"] == "edges/s"
     assert d["config"]["workload"].startswith("ppi:")  # BASELINE.json's metric workload
     head = d["headline_detail"]
@@ -281,7 +292,7 @@ def test_rccl_exchange_one_rank():
         assert d[k] <= 1e-5 + 1e-5 * d[f"scale{k}"], d
 
 
-def test_bench_dist_one_rank_rccl():
+def test_bench_dist_one_rank_rccl(tmp_path):
     """``bench.py --dist`` at one rank (no torchrun): the multi-GPU bench path
     with its all-gather strategies issued over a one-rank RCCL group, the
     PPI-shape headline, and the check against the one-GPU forward."""
@@ -293,12 +304,15 @@ def test_bench_dist_one_rank_rccl():
     env = {k: v for k, v in os.environ.items()
            if k not in ("MASTER_ADDR", "MASTER_PORT", "RANK", "WORLD_SIZE", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, "bench.py", "--dist", "--dist-workloads", "ppi",
-                        "--no-weak", "--steps", "6", "--warmup", "2"], cwd=root, env=env,
+                        "--no-weak", "--steps", "6", "--warmup", "2",
+                        "--detail-out", str(tmp_path / "detail.json")], cwd=root, env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
-    assert len(lines) == 1, r.stdout[-2000:]
-    d = json.loads(lines[0])
+    line = _one_line(r.stdout)
+    for k in ("metric", "value", "ms_per_step", "unit", "scaling"):
+        assert k in line, k
+    assert line["scaling"] == "strong"
+    d = json.load(open(tmp_path / "detail.json"))
     assert d["n_gpus"] == 1 and d["config"]["workload"].startswith("ppi:")
     assert "RCCL" in d["config"]["exchange"]
     head = d["headline_detail"]
@@ -306,3 +320,34 @@ def test_bench_dist_one_rank_rccl():
     ag = d["allgather"] if d["allgather"] is not None else head
     assert ag["collective_ms"] > 0
     assert ag["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * ag["check"]["max_abs_ref"]
+
+
+def test_bench_single_gpu_line(tmp_path):
+    """``bench.py`` at N = 1 (extra workloads, PMC, training and the rank
+    emulation off, to keep it short): exactly one stdout line under the
+    driver's 8 KB budget, carrying the required keys, ``roofline`` and
+    ``cpu_baseline``; the full detail goes to the file (a 29.8 KB
+    line was not parsed)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "bench.py", "--workloads", "", "--no-pmc", "--no-train",
+                        "--emulate-ranks", "", "--steps", "5", "--warmup", "2",
+                        "--detail-out", str(tmp_path / "detail.json")], cwd=root,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _one_line(r.stdout)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in line, k
+    assert line["n_gpus"] == 1 and line["steps"] == 5 and line["scaling"] == "strong"
+    roof = line["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in roof, k
+    assert 0 < roof["frac"] <= 1 and roof["unit"] == "GB/s"
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"]
+    d = json.load(open(tmp_path / "detail.json"))
+    assert d["roofline"]["kernel_ms"] > 0

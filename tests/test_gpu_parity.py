@@ -358,11 +358,12 @@ def test_sliced_default_with_unaligned_x_view():
 
 @pytest.mark.parametrize("fin", [50, 128, 200])
 def test_projection_non_finite_inputs(fin):
-    """Contract for non-finite x (include/gat_amd.h, gat_project): rows
-    without a non-finite value are unaffected (no leak into other rows through
-    clamped or padded loads), and every Wh / s_dst entry the fp64 reference
-    makes non-finite is non-finite here too (the split-bf16 kernels, fin > 64,
-    give NaN where the reference gives +/-Inf: Inf - bf16(Inf) is NaN)."""
+    """Non-finite x (include/gat_amd.h, gat_project): rows without a
+    non-finite value are unaffected (no leak into other rows through clamped
+    or padded loads), and the rows with one equal the reference's fp32
+    ``Linear`` (GAT.py:43-45) — +Inf, -Inf and NaN in the same places, for the
+    fp32-MFMA kernel (fin <= 64) and the split-bf16 ones (fin > 64), whose
+    correction products of an infinite x are dropped (split_sum)."""
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer
     from atmlgraphattentionnetworks_amd.layer import alloc_table, project
     d = dev()
@@ -371,10 +372,12 @@ def test_projection_non_finite_inputs(fin):
     layer = GraphAttentionLayer(fin, F, num_heads=H, concat=True).to(d).eval()
     x = torch.randn(n, fin, device=d)
     clean = x.clone()
-    bad_rows = [0, 17, 351, n - 1]
+    bad_rows = [0, 17, 351, 500, n - 1]
     x[0, 3] = float("inf")
     x[17, fin - 1] = float("-inf")
     x[351, fin // 2] = float("nan")
+    x[500, 1] = float("inf")
+    x[500, fin - 2] = float("-inf")  # Inf - Inf: NaN in the reference
     x[n - 1, 0] = float("inf")
     pp = layer.packed()
     with torch.no_grad():
@@ -384,11 +387,70 @@ def test_projection_non_finite_inputs(fin):
     good[bad_rows] = False
     assert torch.equal(t_bad.wh[good], t_ok.wh[good])
     assert torch.equal(sd_bad[good], sd_ok[good])
-    w64 = pp.w.double()
-    ref = x.double() @ w64.T + pp.b.double()
-    ours = t_bad.wh[:, :H * F]
+    # the reference's own per-head Linears on the host, fp32 (GAT.py:43-45)
+    lin = torch.nn.functional.linear
+    xc = x.cpu()
+
+    def host(p):
+        return p.detach().cpu()
+    with torch.no_grad():
+        wh_ref = torch.cat([lin(xc, host(layer.ws[h].weight), host(layer.ws[h].bias))
+                            for h in range(H)], 1)
+        sd_ref = torch.cat([lin(wh_ref[:, h * F:(h + 1) * F], host(layer.attentions2[h].weight),
+                                host(layer.attentions2[h].bias)) for h in range(H)], 1)
+    ours = t_bad.wh[:, :H * F].cpu()
     for r in bad_rows:
-        nf = ~torch.isfinite(ref[r])
-        assert bool(nf.any())
-        assert not bool(torch.isfinite(ours[r][nf]).any()), (r, ours[r])
-        assert not bool(torch.isfinite(sd_bad[r]).any())
+        assert not bool(torch.isfinite(wh_ref[r]).any())
+        torch.testing.assert_close(ours[r], wh_ref[r], equal_nan=True, atol=0, rtol=0)
+        # s_dst: non-finite in the same places with the same infinities
+        a, b = sd_bad[r].cpu(), sd_ref[r]
+        assert torch.equal(torch.isnan(a), torch.isnan(b)), (r, a, b)
+        assert torch.equal(a[torch.isinf(b)], b[torch.isinf(b)]), (r, a, b)
+
+
+@pytest.mark.parametrize("edges", [60000, 400000])
+def test_layer_copy_and_pickle_after_eval_forward(edges):
+    """the eval forward's cached plans (workspaces, raw device
+    pointers, the bound ctypes call) live in a side table keyed weakly by the
+    layer, not in its __dict__: deepcopy and pickle of a layer that has run
+    work, the copies own their workspaces (the original freed first), and a
+    cached plan does not keep the graph alive.  Short rows (the bound
+    gat_layer_forward call) and long rows (the sliced table)."""
+    import copy
+    import gc
+    import pickle
+    import weakref
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, get_csr
+    from atmlgraphattentionnetworks_amd.layer import _eval_plans
+    from atmlgraphattentionnetworks_amd.synthetic import uniform_graph
+    d = dev()
+    torch.manual_seed(0)
+    n = 3000
+    layer = GraphAttentionLayer(50, 8, num_heads=8, concat=True).to(d).eval()
+    with torch.no_grad():
+        layer.bias.normal_()
+    x = torch.randn(n, 50, device=d)
+    ei = uniform_graph(n, edges, seed=4, device=d)
+    with torch.no_grad():
+        y0 = layer(x, ei)
+        y0b = layer(x, ei)  # the second workspace of the ping-pong pair
+    assert torch.equal(y0, y0b)
+    assert "_eval_plans" not in layer.__dict__ and len(_eval_plans[layer]) == 1
+    cp = copy.deepcopy(layer)
+    blob = pickle.dumps(layer)  # our own bytes, loaded back below
+    del layer
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    junk = torch.full((64 << 20,), float("nan"), device=d)  # reuse the freed memory
+    ld = pickle.loads(blob)
+    with torch.no_grad():
+        for m in (cp, ld):
+            for _ in range(3):
+                assert torch.equal(m(x, ei), y0)
+    del junk
+    # a cached plan holds the graph weakly: dropping the graph frees it
+    csr_ref = weakref.ref(get_csr(ei, n, d).rowptr)
+    del ei
+    gc.collect()
+    assert csr_ref() is None

@@ -152,3 +152,35 @@ def test_summarize_matches_reference_formula():
     import numpy as np
     assert s["mean"] == pytest.approx(0.6)
     assert s["ci95"] == pytest.approx(1.96 * np.sqrt(np.var([0.5, 0.7, 0.6])) / np.sqrt(3))
+
+
+def test_compact_bench_line_fits_driver_budget():
+    """The N = 1 line built from round 3's full 29.8 KB result (the one the
+    driver could not parse) is under the budget and keeps the required keys,
+    the roofline and the CPU baseline."""
+    import json
+    import os
+    from atmlgraphattentionnetworks_amd.benchline import LINE_BUDGET, REQUIRED, compact_single
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    full = json.load(open(os.path.join(root, "profiles", "r03", "bench_default.json")))
+    assert len(json.dumps(full)) > 20000
+    line = compact_single(full, "gpurun_out/bench_detail.json")
+    s = json.dumps(line)
+    assert len(s) <= LINE_BUDGET
+    for k in REQUIRED:
+        assert k in line, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in line["roofline"]
+    assert line["cpu_baseline"]["cores"] == 16 and line["cpu_baseline"]["kind"] == "port"
+    assert line["multi_gpu_emulated"]["reddit"]["allgather_P8"]["bound"] > 1
+
+
+def test_compact_line_drops_optional_keys_first():
+    from atmlgraphattentionnetworks_amd.benchline import REQUIRED, fit
+    line = {k: 1 for k in REQUIRED}
+    line["big"] = "x" * 10000
+    line["small"] = 2
+    out = fit(line, ("big", "small"), budget=500)
+    assert "big" not in out and out["small"] == 2 and all(k in out for k in REQUIRED)
+    out = fit({**line, "other": "y" * 10000}, ("big",), budget=500)
+    assert "truncated" in out and all(k in out for k in REQUIRED)

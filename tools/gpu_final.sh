@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-3 evidence: full GPU suite, smoke, the default bench line, the same
+# Round evidence: full GPU suite, smoke, the default bench line, the same
 # command under rocprofv3 --kernel-trace --stats, the PPI-only bench under
 # rocprofv3 (headline kernel stats), and the multi-GPU rehearsal at world 1.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-TAG=${1:-r03final}
+TAG=${1:-final}
 mkdir -p gpurun_out
 PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 900 $PYT -m gpu tests > gpurun_out/pytest_full_${TAG}.log 2>&1 &&
