@@ -773,8 +773,11 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         int pipe = (u == 16 && vv == 2) ? 1 : 0;
         if (const char* ep = knob("GAT_EDGE_PIPE")) pipe = std::atoi(ep);
         // two lane groups per row (the grid doubles inside launch_edge_fused):
-        // GAT_EDGE_SPLIT = 2 (A/B knob); rows that run segment passes (er.load /
-        // store_lt) and the kink-sum forward keep one group
+        // GAT_EDGE_SPLIT = 2 (A/B knob); the kink-sum forward and the pipelined
+        // kernel keep one group.  Segment passes (er.load / store_lt: hub
+        // segments, the sharded chunk passes) DO take S = 2/4: the carried
+        // (m, l, acc) state is loaded into group 0, merged across the groups in
+        // registers, and stored by group 0.
         // Default: launches of fewer than ~4 waves per SIMD (a rank's share of a
         // small graph: PPI at P = 4 / 8 edge passes 14.2 -> 11.3 / 13.3 -> 9.0 us,
         // tools/emu_probe.py) — there the per-row chain of dependent chunk loads

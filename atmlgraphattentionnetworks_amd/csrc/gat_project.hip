@@ -72,10 +72,12 @@ __global__ __launch_bounds__(256) void k_project(
         float xa[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-            // value used unconditionally (x 0/1 mask), so the load is never
-            // sunk into a branch with its own vmcnt(0); padded k: x * 0
+            // value used unconditionally (a select), so the load is never sunk
+            // into a branch with its own vmcnt(0); padded k and rows past n: 0
+            // (a select, not x * 0: an infinite x would give NaN)
             const int kk = k0 + 4 * s + kq;
-            xa[s] = xr[min(kk, fin - 1)] * (kk < fin ? xs : 0.f);
+            const float v = xr[min(kk, fin - 1)];
+            xa[s] = (kk < fin && xs != 0.f) ? v : 0.f;
         }
         __syncthreads();
         const int ksteps = min(KS, (fin - k0 + 3) / 4);
@@ -573,8 +575,11 @@ __global__ __launch_bounds__(256) void k_project_x3(
     auto stage = [&](int k0, const vec (&xn)[XL], const vec (&wn)[WL]) {
 #pragma unroll
         for (int q = 0; q < XL; ++q) {
+            // k past fin: the clamped load holds real x of this row, which must
+            // not meet the zeroed W (an infinite x would give Inf * 0 = NaN)
             const int e = (tid + NTH * q) * LW;
-            *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) = xn[q];
+            *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) =
+                k0 + e % BK < fin ? xn[q] : vec{};
         }
 #pragma unroll
         for (int q = 0; q < WL; ++q) {
@@ -859,12 +864,16 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
         for (int s = 0; s < KS; ++s) {
             float f[8];
 #pragma unroll
-            for (int q = 0; q < NL; ++q)
+            for (int q = 0; q < NL; ++q) {
+                // k past fin (clamped loads of this row's real x) meets zero W:
+                // zero it, so an infinite x cannot give Inf * 0 = NaN
+                const bool kin = 32 * s + 8 * kq + LW * q < fin;
 #pragma unroll
                 for (int j = 0; j < LW; ++j) {
-                    if constexpr (LW == 1) f[q] = xr[s][q];
-                    else f[q * LW + j] = xr[s][q][j];
+                    if constexpr (LW == 1) f[q] = kin ? xr[s][q] : 0.f;
+                    else f[q * LW + j] = kin ? xr[s][q][j] : 0.f;
                 }
+            }
             split3_x8(f32x4{f[0], f[1], f[2], f[3]}, f32x4{f[4], f[5], f[6], f[7]}, x1[s],
                       x2[s], x3[s]);
         }

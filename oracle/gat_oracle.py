@@ -52,6 +52,7 @@ __all__ = [
     "propagate",
     "gat_layer_forward",
     "gat_layer_forward_from_state",
+    "gat_layer_forward_rows",
     "closed_form_forward",
     "init_reference_params",
     "gat_layer_forward_differentiable",
@@ -119,6 +120,20 @@ def propagate(edge_index: torch.Tensor, x: torch.Tensor, attention_vals, num_nod
     return agg
 
 
+def _project_heads(x, ws_weight, ws_bias, att1_weight, att1_bias, att2_weight, att2_bias):
+    """``GAT.py:42-52``: the head loop of Linears, stack/transpose."""
+    transformed, a1s, a2s = [], [], []
+    for h in range(len(ws_weight)):
+        t = torch.nn.functional.linear(x, ws_weight[h], ws_bias[h])
+        transformed.append(t)
+        a1s.append(torch.nn.functional.linear(t, att1_weight[h], att1_bias[h]))
+        a2s.append(torch.nn.functional.linear(t, att2_weight[h], att2_bias[h]))
+    transformed = torch.transpose(torch.stack(transformed), 0, 1)
+    a1 = torch.stack(a1s).squeeze(-1).T
+    a2 = torch.stack(a2s).squeeze(-1).T
+    return transformed, a1, a2
+
+
 def gat_layer_forward(x: torch.Tensor, edge_index: torch.Tensor,
                       ws_weight: Sequence[torch.Tensor], ws_bias: Sequence[torch.Tensor],
                       att1_weight: Sequence[torch.Tensor], att1_bias: Sequence[torch.Tensor],
@@ -128,16 +143,18 @@ def gat_layer_forward(x: torch.Tensor, edge_index: torch.Tensor,
     with torch.no_grad():
         n = x.size(0)
         edge_ind = add_self_loops(edge_index, n)
-        transformed, a1s, a2s = [], [], []
-        for h in range(len(ws_weight)):
-            t = torch.nn.functional.linear(x, ws_weight[h], ws_bias[h])
-            transformed.append(t)
-            a1s.append(torch.nn.functional.linear(t, att1_weight[h], att1_bias[h]))
-            a2s.append(torch.nn.functional.linear(t, att2_weight[h], att2_bias[h]))
-        transformed = torch.transpose(torch.stack(transformed), 0, 1)
-        a1 = torch.stack(a1s).squeeze(-1).T
-        a2 = torch.stack(a2s).squeeze(-1).T
+        transformed, a1, a2 = _project_heads(x, ws_weight, ws_bias, att1_weight, att1_bias,
+                                             att2_weight, att2_bias)
         return propagate(edge_ind, transformed, (a1, a2), n, concat, negative_slope) + bias
+
+
+def _state_params(state: Dict[str, torch.Tensor], H: int):
+    g = lambda k: state[k].detach().cpu()
+    return ([g(f"ws.{h}.weight") for h in range(H)], [g(f"ws.{h}.bias") for h in range(H)],
+            [g(f"attentions1.{h}.weight") for h in range(H)],
+            [g(f"attentions1.{h}.bias") for h in range(H)],
+            [g(f"attentions2.{h}.weight") for h in range(H)],
+            [g(f"attentions2.{h}.bias") for h in range(H)])
 
 
 def gat_layer_forward_from_state(state: Dict[str, torch.Tensor], x: torch.Tensor,
@@ -145,14 +162,41 @@ def gat_layer_forward_from_state(state: Dict[str, torch.Tensor], x: torch.Tensor
                                  negative_slope: float = 0.2) -> torch.Tensor:
     """Same as :func:`gat_layer_forward`, parameters taken from a reference
     ``state_dict`` (keys ``ws.{h}.weight`` … ``bias``, ``GAT.py:16-35``)."""
-    g = lambda k: state[k].detach().cpu()
-    H = num_heads
-    return gat_layer_forward(
-        x.detach().cpu(), edge_index.detach().cpu(),
-        [g(f"ws.{h}.weight") for h in range(H)], [g(f"ws.{h}.bias") for h in range(H)],
-        [g(f"attentions1.{h}.weight") for h in range(H)], [g(f"attentions1.{h}.bias") for h in range(H)],
-        [g(f"attentions2.{h}.weight") for h in range(H)], [g(f"attentions2.{h}.bias") for h in range(H)],
-        g("bias"), concat, negative_slope)
+    return gat_layer_forward(x.detach().cpu(), edge_index.detach().cpu(),
+                             *_state_params(state, num_heads), state["bias"].detach().cpu(),
+                             concat, negative_slope)
+
+
+def gat_layer_forward_rows(state: Dict[str, torch.Tensor], x: torch.Tensor,
+                           edge_index: torch.Tensor, rows: torch.Tensor, num_heads: int,
+                           concat: bool, negative_slope: float = 0.2,
+                           batch: int = 1024) -> torch.Tensor:
+    """``GAT.py:37-67`` for the target rows ``rows`` only, in batches: the
+    projection (``GAT.py:42-52``) over all N nodes, as the reference does, then
+    per batch the message / segmented softmax / scatter-add (``GAT.py:53-67``)
+    over exactly those rows' in-edges, in ``edge_index`` order, each followed
+    by the row's self-loop (``add_self_loops`` appends every node's loop after
+    all original edges, ``GAT.py:38``, so a row's loop is its last in-edge).
+    A row's output depends only on its own in-edges, so this equals
+    ``gat_layer_forward_from_state(...)[rows]`` with the same per-row op
+    order, while holding [E_batch, H, F] instead of the [E', H, F] message
+    tensor (29 GB at Reddit scale).  Returns [len(rows), width]."""
+    with torch.no_grad():
+        x = x.detach().cpu()
+        ei = edge_index.detach().cpu()
+        rows = rows.detach().cpu().long()
+        n = x.size(0)
+        transformed, a1, a2 = _project_heads(x, *_state_params(state, num_heads))
+        bias = state["bias"].detach().cpu()
+        outs = []
+        for b0 in range(0, rows.numel(), batch):
+            rb = rows[b0:b0 + batch]
+            sub = ei[:, torch.isin(ei[1], rb)]
+            loops = rb.unique().unsqueeze(0).repeat(2, 1)
+            agg = propagate(torch.cat([sub, loops], dim=1), transformed, (a1, a2), n, concat,
+                            negative_slope)
+            outs.append(agg[rb] + bias)
+        return torch.cat(outs)
 
 
 def closed_form_forward(state: Dict[str, torch.Tensor], x, edge_index, num_heads: int,

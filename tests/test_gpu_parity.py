@@ -356,8 +356,9 @@ def test_sliced_default_with_unaligned_x_view():
     assert rc == _lib.GAT_EUNSUPPORTED
 
 
-@pytest.mark.parametrize("fin", [50, 128, 200])
-def test_projection_non_finite_inputs(fin):
+@pytest.mark.parametrize("fin,kernel", [(50, None), (50, "tiled"), (128, None), (100, None),
+                                        (200, None), (602, None), (130, "tiled")])
+def test_projection_non_finite_inputs(fin, kernel, monkeypatch):
     """Non-finite x (include/gat_amd.h, gat_project): rows without a
     non-finite value are unaffected (no leak into other rows through clamped
     or padded loads), and the rows with one equal the reference's fp32
@@ -365,7 +366,11 @@ def test_projection_non_finite_inputs(fin):
     fp32-MFMA kernel (fin <= 64) and the split-bf16 ones (fin > 64), whose
     correction products of an infinite x are dropped (split_sum)."""
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    from atmlgraphattentionnetworks_amd import tuning
     from atmlgraphattentionnetworks_amd.layer import alloc_table, project
+    if kernel is not None:
+        monkeypatch.setenv("GAT_PROJ_KERNEL", kernel)
+    tuning.reload()
     d = dev()
     torch.manual_seed(0)
     H, F, n = 8, 8, 700

@@ -84,3 +84,22 @@ def test_dropout_mask_restatement_properties():
     # edges (src->dst): 1->1, 2->0, 0->1, loops 0->0, 1->1, 2->2
     # rows: 0: [0->0 (loop), 2->0]; 1: [0->1, 1->1 (input), 1->1 (loop)]; 2: [2->2]
     assert csr_positions(ei, 3).tolist() == [3, 1, 2, 0, 4, 5]
+
+
+@pytest.mark.parametrize("concat,H", [(True, 8), (False, 4)])
+def test_oracle_rows_equals_full_forward(concat, H):
+    """gat_layer_forward_rows (the sampled-row oracle the Reddit-scale GPU
+    tests use) gives exactly the full oracle's rows: same projection, and each
+    row's in-edges in the same order with its self-loop last."""
+    from oracle import gat_layer_forward_from_state, gat_layer_forward_rows, init_reference_params
+    g = torch.Generator().manual_seed(3)
+    n, e = 900, 20000
+    ei = torch.stack([torch.randint(0, n, (e,), generator=g), torch.randint(0, n, (e,), generator=g)])
+    ei[:, :50] = torch.tensor([[5] * 50, [5] * 50])  # pre-existing loops and multi-edges
+    x = torch.randn(n, 20, generator=g)
+    state = init_reference_params(20, 8, H, concat, seed=1)
+    state["bias"] = torch.randn(state["bias"].shape, generator=g)
+    full = gat_layer_forward_from_state(state, x, ei, H, concat)
+    rows = torch.cat([torch.tensor([5, 0, n - 1, 5]), torch.randperm(n, generator=g)[:300]])
+    part = gat_layer_forward_rows(state, x, ei, rows, H, concat, batch=128)
+    torch.testing.assert_close(part, full[rows], atol=0, rtol=0)
