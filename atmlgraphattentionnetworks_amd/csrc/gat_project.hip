@@ -520,8 +520,8 @@ __device__ __forceinline__ void split3_x8(f32x4 a, f32x4 b, bf16x8& h1, bf16x8& 
     }
 }
 
-template <int NT, int LW, int RG, int PD>
-__global__ __launch_bounds__(256) void k_project_x3(
+template <int NT, int LW, int RG, int PD, int MINB = 1>
+__global__ __launch_bounds__(256, MINB) void k_project_x3(
     const float* __restrict__ X, int n, int fin,
     const float* __restrict__ W, const float* __restrict__ bW,
     const float* __restrict__ a1, const float* __restrict__ c1,
@@ -1274,6 +1274,17 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         // fragments with one chunk in flight
         int bm = lw == 4 ? 64 : 128;
         if (const char* v = knob("GAT_PROJ_BM")) bm = std::atoi(v);
+        // GAT_PROJ_X3V (A/B knob): block shape and register bound of k_project_x3.
+        // "b64p1": 64 rows, one chunk in flight; "b64p1w3": the same bounded to 3
+        // workgroups per CU; "b128w2": 128 rows bounded to 2 workgroups per CU
+        // (k_project_x3<.., 2, 1> unbounded takes 308 registers: one wave per SIMD)
+        int x3v = 0;
+        if (const char* v = knob("GAT_PROJ_X3V")) {
+            if (std::strcmp(v, "b64p1") == 0) x3v = 1;
+            else if (std::strcmp(v, "b64p1w3") == 0) x3v = 2;
+            else if (std::strcmp(v, "b128w2") == 0) x3v = 3;
+            else if (std::strcmp(v, "b64w2") == 0) x3v = 4;
+        }
 #ifdef GAT_AB_KERNELS
 #define GAT_PIPE2_FP32(NT, LWV)                                                                \
         hipLaunchKernelGGL((k_project_pipe2<NT, LWV>), gp, bp, 0, st, x, n, fin, w, b, a_src, \
@@ -1282,8 +1293,16 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #else
 #define GAT_PIPE2_FP32(NT, LWV) (void)gp
 #endif
+#define GAT_X3V(NT, LWV, RGV, PDV, MB, BMV)                                                   \
+    hipLaunchKernelGGL((k_project_x3<NT, LWV, RGV, PDV, MB>), dim3((n + BMV - 1) / BMV), bp, 0, \
+                       st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,      \
+                       ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt)
 #define GAT_PIPE2(NT, LWV)                                                                     \
-    if (x3 && bm == 128)                                                                       \
+    if (x3 && x3v == 1) GAT_X3V(NT, LWV, 1, 1, 1, 64);                                         \
+    else if (x3 && x3v == 2) GAT_X3V(NT, LWV, 1, 1, 3, 64);                                    \
+    else if (x3 && x3v == 3) GAT_X3V(NT, LWV, 2, 1, 2, 128);                                   \
+    else if (x3 && x3v == 4) GAT_X3V(NT, LWV, 1, 2, 2, 64);                                    \
+    else if (x3 && bm == 128)                                                                  \
         hipLaunchKernelGGL((k_project_x3<NT, LWV, 2, 1>), dim3((n + 127) / 128), bp, 0, st,    \
                            x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,     \
                            ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt);       \
@@ -1304,6 +1323,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #undef GAT_PIPE2_LW
 #undef GAT_PIPE2
 #undef GAT_PIPE2_FP32
+#undef GAT_X3V
         return status_of(hipGetLastError());
     }
     if (sliced) return GAT_EUNSUPPORTED;  // the kernels below write row-major Wh only

@@ -69,7 +69,7 @@ def main():
         hf = H * F
         epr = w.num_edges // n_full + 1
         slices = 2 if (hf == 64 and epr >= 16 and w.concat) else 1
-        stream = torch.cuda.current_stream()
+        stream = torch.cuda.current_stream()  # (timing events; launches use the current one)
         outs = []
         for e in envs:
             wh = torch.empty(n * ((hf + 3) // 4 * 4), device=dev)
@@ -79,18 +79,19 @@ def main():
 
         def launch(i):
             wh, sd, ss = outs[i]
+            st = torch.cuda.current_stream().cuda_stream  # the capture stream inside a graph
             if slices > 1:
                 rc = lib.gat_project_sliced(x.data_ptr(), n, w.in_channels, pp.w.data_ptr(),
                                             pp.b.data_ptr(), pp.a_src.data_ptr(),
                                             pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
                                             pp.c_dst.data_ptr(), H, F, slices, wh.data_ptr(), n,
-                                            0, H, sd.data_ptr(), stream.cuda_stream)
+                                            0, H, sd.data_ptr(), st)
             else:
                 rc = lib.gat_project(x.data_ptr(), n, w.in_channels, pp.w.data_ptr(),
                                      pp.b.data_ptr(), pp.a_src.data_ptr(), pp.c_src.data_ptr(),
                                      pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), H, F,
                                      wh.data_ptr(), (hf + 3) // 4 * 4, ss.data_ptr(), H,
-                                     sd.data_ptr(), stream.cuda_stream)
+                                     sd.data_ptr(), st)
             if rc:
                 raise RuntimeError(f"projection rc={rc}")
 
