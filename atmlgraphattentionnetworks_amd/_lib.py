@@ -18,7 +18,7 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 7
+GAT_ABI_VERSION = 8
 GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
 GAT_SEG_LOAD = 1
 GAT_SEG_STORE = 2
@@ -47,6 +47,9 @@ SIGNATURES = {
     "gat_project_sliced": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                     _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_int,
                                     _c_vp, _c_vp]),
+    "gat_project_chunked": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                     _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int, _c_int, _c_ll,
+                                     _c_vp, _c_vp]),
     "gat_edge_aggregate_sliced": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
                                            _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_float,
                                            _c_vp, _c_vp, _c_int, _c_vp]),

@@ -520,6 +520,21 @@ __device__ __forceinline__ void split3_x8(f32x4 a, f32x4 b, bf16x8& h1, bf16x8& 
     }
 }
 
+// Row chunks (gridDim.y > 1, gat_project_chunked): blockIdx.y = c projects rows
+// [c crows, (c + 1) crows) of x into the Wh block that starts cjump floats
+// further per chunk (a rank's chunk slots of the multi-GPU node table, one
+// launch for all of them); s_dst and s_src rows stay contiguous.
+#define GAT_ROW_CHUNKS()                                                          \
+    if (gridDim.y > 1) {                                                          \
+        const int cy_ = (int)blockIdx.y;                                          \
+        X += (size_t)cy_ * (size_t)crows * (size_t)fin;                           \
+        Wh += (size_t)cy_ * (size_t)cjump;                                        \
+        s_dst += (size_t)cy_ * (size_t)crows * (size_t)H;                         \
+        if (Ss != nullptr) Ss += (size_t)cy_ * (size_t)crows * (size_t)ld_s;      \
+        n = min(crows, n - cy_ * crows);                                          \
+        if (n <= 0) return;                                                       \
+    }
+
 template <int NT, int LW, int RG, int PD, int MINB = 1>
 __global__ __launch_bounds__(256, MINB) void k_project_x3(
     const float* __restrict__ X, int n, int fin,
@@ -527,7 +542,9 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
     const float* __restrict__ a1, const float* __restrict__ c1,
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
-    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt) {
+    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt, int crows,
+    long long cjump) {
+    GAT_ROW_CHUNKS();
     // RG 16-row groups per wave, 4 waves: BM = 64 RG rows per block
     constexpr int BK = 64, BN = NT * 16, NTH = 256, BM = 64 * RG;
     constexpr int XS = BK + 4, WSB = BK + 8, OS = BN + 4;
@@ -762,7 +779,9 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
     const float* __restrict__ a1, const float* __restrict__ c1,
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
-    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt) {
+    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt, int crows,
+    long long cjump) {
+    GAT_ROW_CHUNKS();
     constexpr int BN = NT * 16, KP = KS * 32;  // padded K
     constexpr int WSB = KP + 8, OS = BN + 4;
     constexpr int NL = 8 / LW;                  // loads per 8-float fragment
@@ -987,7 +1006,9 @@ __global__ __launch_bounds__(256) void k_project_wk(
     const float* __restrict__ a2, const float* __restrict__ c2,
     int H, int F, int HF, float* __restrict__ Wh, int ld_wh,
     float* __restrict__ Ss, int ld_s, float* __restrict__ s_dst,
-    int slice_w, long long slice_stride, int store_wt) {
+    int slice_w, long long slice_stride, int store_wt, int crows,
+    long long cjump) {
+    GAT_ROW_CHUNKS();
     constexpr int BM = 64, BN = NT * 16;
     constexpr int OS = BN + 4;  // output-tile stride: float4-aligned rows, no write conflicts
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1154,7 +1175,8 @@ extern "C" {
 static int project_impl(const float* x, int n, int fin, const float* w, const float* b,
                         const float* a_src, const float* c_src, const float* a_dst,
                         const float* c_dst, int heads, int f, int slices, float* wh, int ld_wh,
-                        float* s_src, int ld_s, float* s_dst, void* stream, int n_table = 0) {
+                        float* s_src, int ld_s, float* s_dst, void* stream, int n_table = 0,
+                        int crows = 0, long long cjump = 0) {
     if (n < 0 || fin < 0 || heads <= 0 || f <= 0 || slices <= 0) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
@@ -1165,12 +1187,16 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     } else if (ld_wh < round_up4(hf) || (ld_wh & 3) || ld_s < heads) {
         return GAT_EINVAL;
     }
-    if (sliced && n_table < n) return GAT_EINVAL;
+    if (sliced && n_table < (crows > 0 ? std::min(crows, n) : n)) return GAT_EINVAL;
     if (n == 0) return GAT_OK;
+    // row chunks (gat_project_chunked): ny launches' worth of rows in one grid
+    if (crows < 0 || (crows > 0 && (crows % 64 != 0 || !sliced))) return GAT_EINVAL;
+    const int ny = crows > 0 ? (n + crows - 1) / crows : 1;
+    const int nr = crows > 0 ? std::min(crows, n) : n;  // rows per grid slice
     const int slice_w = sliced ? ld_wh : round_up4(hf);
     const long long slice_stride = sliced ? (long long)n_table * ld_wh : 0;
     hipStream_t st = (hipStream_t)stream;
-    const dim3 grid((n + 63) / 64), block(256);
+    const dim3 grid((nr + 63) / 64, ny), block(256);
     const int nt = (hf + 15) / 16;
     const int store_wt = store_wt_on();  // Wh / scores stored write-through
     // GAT_PROJ_KERNEL (A/B knob, tools/tests): "wk" (whole K in LDS; the
@@ -1193,16 +1219,17 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
         const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
         const int ks = fin <= 32 ? 1 : fin <= 64 ? 2 : 4;
-        const long long tiles = (n + 15) / 16;
+        const long long tiles = (nr + 15) / 16;
         // persistent beyond the workgroups one CU holds at once (each wave loops
         // over tiles): 3 per CU for K <= 64 (45 KB of LDS, <= 168 VGPRs), else 2
         int wg_cu = ks <= 2 ? 3 : 2;
         if (const char* v = knob("GAT_PROJ_WRES_WGS")) wg_cu = std::max(1, std::atoi(v));
-        const int grid_w = (int)std::min<long long>((tiles + 3) / 4, 256LL * wg_cu);
+        const int grid_w = (int)std::max<long long>(
+            1, std::min<long long>((tiles + 3) / 4, 256LL * wg_cu / ny));
 #define GAT_WRES(NTV, LWV, KSV)                                                               \
-    hipLaunchKernelGGL((k_project_wres<NTV, LWV, KSV>), dim3(grid_w), dim3(256), 0, st, x, n, \
-                       fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src,  \
-                       ld_s, s_dst, slice_w, slice_stride, store_wt)
+    hipLaunchKernelGGL((k_project_wres<NTV, LWV, KSV>), dim3(grid_w, ny), dim3(256), 0, st, x, \
+                       n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh,     \
+                       s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, cjump)
 #define GAT_WRES_KS(NTV, LWV)                                          \
     switch (ks) {                                                      \
         case 1: GAT_WRES(NTV, LWV, 1); break;                          \
@@ -1235,11 +1262,12 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         if (direct)                                                                           \
             hipLaunchKernelGGL((k_project_wk<NT, true>), grid, block, wk_lds, st, x, n, fin,  \
                                w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh,     \
-                               s_src, ld_s, s_dst, slice_w, slice_stride, store_wt);          \
+                               s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows,    \
+                               cjump);                                                        \
         else                                                                                  \
             hipLaunchKernelGGL((k_project_wk<NT>), grid, block, wk_lds, st, x, n, fin, w, b,  \
                                a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src,    \
-                               ld_s, s_dst, slice_w, slice_stride, store_wt);                 \
+                               ld_s, s_dst, slice_w, slice_stride, store_wt, crows, cjump);   \
         break;
         switch (nt) {
             GAT_WK_CASE(1) GAT_WK_CASE(2) GAT_WK_CASE(3) GAT_WK_CASE(4)
@@ -1258,7 +1286,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
                          (nt == 1 || nt == 2 || nt == 4) && pow2_f && f <= 16 &&
                          (long long)n * fin < (1LL << 31) && (pk == nullptr || force_pipe);
     if (pipe_ok) {
-        const dim3 gp((n + 127) / 128), bp(256);
+        const dim3 gp((nr + 127) / 128, ny), bp(256);
         const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
         const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
         // split-bf16 matrix cores (k_project_x3) unless GAT_PROJ_X3=0 (A/B knob:
@@ -1267,6 +1295,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #ifdef GAT_AB_KERNELS
         if (const char* v = knob("GAT_PROJ_X3")) x3 = std::atoi(v) != 0;
 #endif
+        if (!x3 && ny > 1) return GAT_EUNSUPPORTED;  // k_project_pipe2 has no row chunks
         // rows per block (GAT_PROJ_BM A/B knob: 64 = one 16-row group per wave,
         // 128 = two, sharing every B fragment)
         // tools/proj_ab.py: 4-float x rows (arxiv) prefer 64 rows per block with two
@@ -1294,23 +1323,25 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #define GAT_PIPE2_FP32(NT, LWV) (void)gp
 #endif
 #define GAT_X3V(NT, LWV, RGV, PDV, MB, BMV)                                                   \
-    hipLaunchKernelGGL((k_project_x3<NT, LWV, RGV, PDV, MB>), dim3((n + BMV - 1) / BMV), bp, 0, \
-                       st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,      \
-                       ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt)
+    hipLaunchKernelGGL((k_project_x3<NT, LWV, RGV, PDV, MB>), dim3((nr + BMV - 1) / BMV, ny), bp, \
+                       0, st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,   \
+                       ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows,     \
+                       cjump)
 #define GAT_PIPE2(NT, LWV)                                                                     \
     if (x3 && x3v == 1) GAT_X3V(NT, LWV, 1, 1, 1, 64);                                         \
     else if (x3 && x3v == 2) GAT_X3V(NT, LWV, 1, 1, 3, 64);                                    \
     else if (x3 && x3v == 3) GAT_X3V(NT, LWV, 2, 1, 2, 128);                                   \
     else if (x3 && x3v == 4) GAT_X3V(NT, LWV, 1, 2, 2, 64);                                    \
     else if (x3 && bm == 128)                                                                  \
-        hipLaunchKernelGGL((k_project_x3<NT, LWV, 2, 1>), dim3((n + 127) / 128), bp, 0, st,    \
-                           x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,     \
-                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt);       \
+        hipLaunchKernelGGL((k_project_x3<NT, LWV, 2, 1>), dim3((nr + 127) / 128, ny), bp, 0,   \
+                           st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, \
+                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, \
+                           cjump);                                                            \
     else if (x3)                                                                               \
-        hipLaunchKernelGGL((k_project_x3<NT, LWV, 1, 2>), dim3((n + 63) / 64), bp, 0, st, x, n, \
-                           fin, w, b, a_src,                                                  \
-                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
-                           slice_w, slice_stride, store_wt);                                  \
+        hipLaunchKernelGGL((k_project_x3<NT, LWV, 1, 2>), dim3((nr + 63) / 64, ny), bp, 0, st,  \
+                           x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,     \
+                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, \
+                           cjump);                                                            \
     else                                                                                       \
         GAT_PIPE2_FP32(NT, LWV)
 #define GAT_PIPE2_LW(NT)                                  \
@@ -1326,7 +1357,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #undef GAT_X3V
         return status_of(hipGetLastError());
     }
-    if (sliced) return GAT_EUNSUPPORTED;  // the kernels below write row-major Wh only
+    if (sliced || ny > 1) return GAT_EUNSUPPORTED;  // the kernels below: row-major Wh, no chunks
     const bool shfl = ((f <= 16 && 16 % f == 0) || (f % 16 == 0)) &&
                       !(pk != nullptr && std::strcmp(pk, "lds") == 0);
 #define GAT_PROJ_CASE(NT)                                                                   \
@@ -1367,6 +1398,19 @@ int gat_project_sliced(const float* x, int n, int fin, const float* w, const flo
     if (s_src == nullptr) ld_s = heads;  // the sliced edge kernel recomputes s_src
     return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
                         heads * f / slices, s_src, ld_s, s_dst, stream, n_table);
+}
+
+int gat_project_chunked(const float* x, int n, int fin, const float* w, const float* b,
+                        const float* a_src, const float* c_src, const float* a_dst,
+                        const float* c_dst, int heads, int f, int slices, float* wh,
+                        int plane_rows, int chunk_rows, long long chunk_stride, float* s_dst,
+                        void* stream) {
+    if (slices <= 1 || heads <= 0 || f <= 0 || (heads * f) % slices != 0 || chunk_rows <= 0 ||
+        plane_rows < chunk_rows || chunk_stride < (long long)slices * plane_rows * (heads * f / slices))
+        return GAT_EINVAL;
+    return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
+                        heads * f / slices, nullptr, heads, s_dst, stream, plane_rows, chunk_rows,
+                        chunk_stride);
 }
 
 }  // extern "C"

@@ -180,6 +180,23 @@ class HipOps:
         _lib.check(rc, "gat_project (shard block)")
 
     @staticmethod
+    def project_chunked(x, pp, heads, f, layout: TableLayout, table, rank: int, s_dst):
+        """All of a rank's rows in ONE launch (gat_project_chunked): row chunk c
+        goes to the rank's block of table chunk c (planes layout only)."""
+        lib = _lib.load()
+        n, fin = x.shape
+        if n == 0:
+            return
+        stream = torch._C._cuda_getCurrentRawStream(x.device.index)
+        rc = lib.gat_project_chunked(
+            x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(),
+            pp.c_src.data_ptr(), pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
+            layout.slices, table.data_ptr() + 4 * layout.block_offset(0, rank),
+            layout.block_rows, layout.block_rows, layout.world * layout.block_floats,
+            s_dst.data_ptr(), stream)
+        _lib.check(rc, "gat_project_chunked (shard)")
+
+    @staticmethod
     def edge_pass(local: LocalCSR, c: int, layout: TableLayout, table, s_dst, pp, bias, heads,
                   f, concat, act, param, out, st_acc, st_ml, flags):
         lib = _lib.load()
@@ -407,6 +424,20 @@ class ShardedGAT:
         self.ops.project_rows(xl[lo:hi], self.pp, self.heads, self.f, lay, self.table,
                               lay.block_offset(c, self.rank), self.s_dst[lo:hi], self.s_scratch)
 
+    def project_all(self, xl) -> None:
+        """Every chunk's projection: one launch over all of the rank's rows
+        where the ops and the table layout allow it (planes, several chunks:
+        a per-chunk launch pays a whole block's latency for 1/K of the rows),
+        else one launch per chunk."""
+        lay = self.layout
+        if (self.exchange == "allgather" and lay.kind == "planes" and self.chunks > 1
+                and hasattr(self.ops, "project_chunked") and lay.block_rows % 64 == 0):
+            self.ops.project_chunked(xl, self.pp, self.heads, self.f, lay, self.table,
+                                     self.rank, self.s_dst)
+            return
+        for c in range(self.chunks):
+            self.project_chunk(xl, c)
+
     def exchange_start(self, c: int):
         if self.exchange != "allgather" or (self.world == 1 and not self.force_exchange):
             return None
@@ -431,10 +462,8 @@ class ShardedGAT:
         if self.exchange == "replicate":
             self.project_chunk(xl, 0)
             return self.edge_pass(0)
-        handles = []
-        for c in range(self.chunks):
-            self.project_chunk(xl, c)
-            handles.append(self.exchange_start(c))
+        self.project_all(xl)
+        handles = [self.exchange_start(c) for c in range(self.chunks)]
         for c in range(self.chunks):
             self.exchanger.wait(handles[c])
             self.edge_pass(c)
@@ -442,8 +471,7 @@ class ShardedGAT:
 
     # split phases, for timing the collective and the compute alone
     def phase_project(self, xl):
-        for c in range(self.chunks):
-            self.project_chunk(xl, c)
+        self.project_all(xl)
 
     def phase_exchange(self):
         hs = [self.exchange_start(c) for c in range(self.chunks)]

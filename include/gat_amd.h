@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 7
+#define GAT_ABI_VERSION 8
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -160,6 +160,23 @@ int gat_project_sliced(const float* x, int n, int fin, const float* w, const flo
                        const float* a_src, const float* c_src, const float* a_dst,
                        const float* c_dst, int heads, int f, int slices, float* wh, int n_table,
                        float* s_src, int ld_s, float* s_dst, void* stream);
+/*
+ * gat_project_chunked (ABI 8): gat_project_sliced for the rows of one rank of
+ * the multi-GPU node table, all of its all-gather chunks in ONE launch.  Rows
+ * [c*chunk_rows, (c+1)*chunk_rows) of x (n rows in total) go to planes of
+ * plane_rows rows starting at wh + c*chunk_stride floats (the table block of
+ * chunk c; plane g at + g*plane_rows*sw); s_dst stays one contiguous [n, heads]
+ * array; s_src is not written.  chunk_rows % 64 == 0, plane_rows >= chunk_rows,
+ * chunk_stride >= slices*plane_rows*sw.  Replaces a per-chunk loop of
+ * gat_project_sliced calls, each of which pays a whole block's latency (a
+ * 9.7k-row chunk of the Reddit shape: ~30 us per launch for 1/3 of the rows).
+ * Results are identical to those calls'.
+ */
+int gat_project_chunked(const float* x, int n, int fin, const float* w, const float* b,
+                        const float* a_src, const float* c_src, const float* a_dst,
+                        const float* c_dst, int heads, int f, int slices, float* wh,
+                        int plane_rows, int chunk_rows, long long chunk_stride, float* s_dst,
+                        void* stream);
 int gat_edge_aggregate_sliced(const int* rowptr, const int* col, const int* row_order,
                               int row_begin, int row_end, const float* wh, int n_table,
                               int slices, const float* a_src, const float* c_src,

@@ -353,3 +353,29 @@ def test_bench_single_gpu_line(tmp_path):
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"]
     d = json.load(open(tmp_path / "detail.json"))
     assert d["roofline"]["kernel_ms"] > 0
+
+
+@pytest.mark.parametrize("P,chunks,fin", [(2, 3, 50), (8, 3, 50), (4, 4, 602), (8, 2, 128)])
+def test_chunked_projection_equals_per_chunk_launches(P, chunks, fin):
+    """gat_project_chunked (one launch for all of a rank's chunk blocks) writes
+    exactly what one gat_project_sliced launch per chunk writes: every table
+    block bit for bit, s_dst too (including the partial last chunk)."""
+    from atmlgraphattentionnetworks_amd import get_csr
+    from atmlgraphattentionnetworks_amd.distributed import ShardedGAT
+    state, x, ei = _small_case(True, n=5000, e=100000, fin=fin)
+    layer = _layer(fin, 8, 8, True, state)
+    csr = get_csr(ei, x.size(0))
+    with torch.no_grad():
+        for rank in range(P):
+            sh = ShardedGAT(layer, csr, P, rank, chunks=chunks, pingpong=False)
+            assert sh.layout.kind == "planes" and sh.chunks == chunks
+            xl = sh.local_x(x)
+            sh.table.fill_(float("nan"))
+            sh.project_all(xl)
+            t1, s1 = sh.table.clone(), sh.s_dst.clone()
+            sh.table.fill_(float("nan"))
+            sh.s_dst.fill_(float("nan"))
+            for c in range(sh.chunks):
+                sh.project_chunk(xl, c)
+            assert torch.equal(torch.nan_to_num(t1, nan=7.0), torch.nan_to_num(sh.table, nan=7.0))
+            assert torch.equal(s1[:sh.n_local], sh.s_dst[:sh.n_local])

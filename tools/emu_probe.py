@@ -4,6 +4,8 @@ under kernel knobs, on one GPU: which edge-kernel schedule suits a rank's
 small share of a graph?
 
     python3 tools/emu_probe.py --workload ppi --ranks 8 --variants "base;GAT_EDGE_U=8"
+
+A variant may set the pseudo-knob chunks=K (all-gather chunks / edge passes).
 """
 import argparse
 import json
@@ -44,17 +46,19 @@ def main():
     out = {}
     with torch.no_grad():
         for spec, env in variants:
+            env = dict(env)
+            chunks = int(env.pop("chunks")) if "chunks" in env else None
             for k in knobs:
                 os.environ.pop(k, None)
             os.environ.update(env)
             tuning.reload()
             for p in [int(v) for v in args.ranks.split(",")]:
-                r = emulate_rank_times(layer, csr, x, p, exchange=args.exchange)
+                r = emulate_rank_times(layer, csr, x, p, exchange=args.exchange, chunks=chunks)
                 out[f"{spec}|P{p}"] = {"max_project_us": r["max_project_ms"] * 1e3,
                                        "max_edge_passes_us": r["max_edge_passes_ms"] * 1e3,
                                        "chunks": r["chunks"]}
     print(json.dumps({"workload": args.workload, "exchange": args.exchange, "results": out},
-                     indent=1))
+                     indent=1), flush=True)
 
 
 if __name__ == "__main__":
