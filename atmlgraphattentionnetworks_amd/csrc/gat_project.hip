@@ -970,6 +970,190 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
 }
 
 // ---------------------------------------------------------------------------
+// Projection for fin in {32, 64, 128} (ogbn-arxiv's 128): k_project_wres's
+// W-resident split-bf16 form, with x streamed through LDS by LDS-DMA
+// (global_load_lds_dwordx4) instead of fragment-shaped loads into registers.
+//
+// A 16-row x tile is one contiguous 16*fin*4-byte run (x 16-B aligned), so
+// each wave fetches its tiles in whole 1-KiB wave-instructions (8 per tile at
+// fin = 128), fully coalesced, into a private ring of NB = 3 tile buffers:
+// tiles i+1 and i+2 are in flight while tile i is computed, with no VGPRs
+// spent on them and no per-element address arithmetic (fragment-shaped loads
+// touch 16 rows x 32 B per instruction: MI355X_MICROARCH / cdna guide measure
+// them at ~2x the TA time of full-line staging).  The LDS image is
+// XOR-swizzled through the SOURCE address (LDS-DMA writes lane-linear): 16-B
+// piece p of row r lands at p ^ (r & 15), so the A/B fragment reads
+// (ds_read_b128, rows cl = 0..15) hit 16 distinct 4-bank groups.
+// Operands swapped as k_project_wk's DIRECT form (A = W fragment, B = x
+// fragment): each lane ends with four consecutive Wh columns of one row and
+// the epilogue stores them straight from registers (proj_direct_epilogue).
+// Ordering: a wave reads only buffers it filled itself, after a counted
+// s_waitcnt vmcnt that retires that tile's LDS-DMA (the two younger tiles'
+// 2 * GLDS DMAs, and any younger stores, may stay in flight); a buffer is
+// refilled one iteration after its fragments were consumed by MFMAs.
+// One workgroup per CU (W planes 52 KB + 4 waves x 3 x 8 KB ring).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef __attribute__((address_space(1))) void* gbl_void_ptr;
+
+template <int NT, int KS, int EXTRA = 0>
+__global__ __launch_bounds__(256, 1) void k_project_wg(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
+    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt, int crows,
+    long long cjump) {
+    GAT_ROW_CHUNKS();
+    constexpr int BN = NT * 16, KP = KS * 32;  // fin == KP
+    constexpr int WSB = KP + 8;
+    constexpr int TILE = 16 * KP;              // floats per x tile
+    constexpr int PIECES = KP / 4;             // 16-B pieces per x row (8, 16 or 32)
+    constexpr int SWM = PIECES < 16 ? PIECES - 1 : 15;
+    constexpr int GLDS = TILE / 256;           // 1-KiB LDS-DMA wave-instructions per tile
+    static_assert(GLDS >= 1 && (PIECES & (PIECES - 1)) == 0, "fin must be 32, 64 or 128");
+    __shared__ __attribute__((aligned(16))) __bf16 wsb[3][BN * WSB];
+    // three separate ring buffers (not one indexed array): the compiler's
+    // waitcnt pass then sees that a fragment read of one buffer cannot alias
+    // the LDS-DMA in flight into the others, and does not wait vmcnt(0)
+    __shared__ __attribute__((aligned(16))) float xr0[4][TILE];
+    __shared__ __attribute__((aligned(16))) float xr1[4][TILE];
+    __shared__ __attribute__((aligned(16))) float xr2[4][TILE];
+    __shared__ __attribute__((aligned(16))) float prm[3 * BN + 2 * 64];
+    float* bs = prm;
+    float* a1s = prm + BN;
+    float* a2s = prm + 2 * BN;
+    float* c1s = prm + 3 * BN;
+    float* c2s = c1s + 64;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int tiles = (n + 15) / 16;
+    const int tstride = gridDim.x * 4;
+    int tile = blockIdx.x * 4 + w;
+    // LDS-DMA of one tile into ring buffer b: unit u = 64 i + lane of the tile
+    // image holds row u / PIECES, stored piece u % PIECES = source piece ^ swizzle
+    auto fetch = [&](int tl, float* dst) {
+        const int t = min(tl, tiles - 1);  // past the end: a harmless reload
+#pragma unroll
+        for (int i = 0; i < GLDS; ++i) {
+            const int u = i * 64 + lane;
+            const int r = u / PIECES, pc = u % PIECES;
+            const int grow = min(t * 16 + r, n - 1);
+            const float* src = X + (size_t)grow * KP + 4 * (pc ^ (r & SWM));
+            // by inline asm: the compiler then does not track these DMAs, so it
+            // never adds its own conservative vmcnt(0) before the ring's fragment
+            // reads (its waits for its own loads can only grow longer, never
+            // shorter); the counted waits below order the reads
+            const unsigned ldst = __builtin_amdgcn_readfirstlane(
+                (unsigned)(uintptr_t)(lds_void_ptr)(dst + i * 256));  // wave-uniform
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(src), "s"(ldst)
+                : "memory");
+        }
+    };
+    fetch(tile, xr0[w]);
+    fetch(tile + tstride, xr1[w]);
+    // W split into three bf16 planes (k_project_wres's loads: unconditional,
+    // clamped, all issued together), zero past HF columns
+    {
+        constexpr int WQ = (BN * KP + 256 * 4 - 1) / (256 * 4);
+        f32x4 wv[WQ];
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) {
+            const int e = (tid + 256 * q) * 4;
+            const int c = min(e / KP, HF - 1), k = e % KP;
+            wv[q] = *reinterpret_cast<const f32x4*>(W + (size_t)c * KP + k);
+        }
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) {
+            const int e = (tid + 256 * q) * 4;
+            if (e < BN * KP) {
+                const int c = e / KP, k = e % KP;
+                const f32x4 v = c < HF ? wv[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+                bf16x2 p1a, p2a, p3a, p1b, p2b, p3b;
+                split3_pair(f32x2{v.x, v.y}, p1a, p2a, p3a);
+                split3_pair(f32x2{v.z, v.w}, p1b, p2b, p3b);
+                const int o = c * WSB + k;
+                *reinterpret_cast<bf16x4*>(&wsb[0][o]) = bf16x4{p1a[0], p1a[1], p1b[0], p1b[1]};
+                *reinterpret_cast<bf16x4*>(&wsb[1][o]) = bf16x4{p2a[0], p2a[1], p2b[0], p2b[1]};
+                *reinterpret_cast<bf16x4*>(&wsb[2][o]) = bf16x4{p3a[0], p3a[1], p3b[0], p3b[1]};
+            }
+        }
+    }
+    if (tid < BN) {
+        const bool ok = tid < HF;
+        const int cc = ok ? tid : 0;
+        const float bv = bW[cc], av1 = a1[cc], av2 = a2[cc];
+        bs[tid] = ok ? bv : 0.f;
+        a1s[tid] = ok ? av1 : 0.f;
+        a2s[tid] = ok ? av2 : 0.f;
+    }
+    if (tid < H) {
+        const float v1 = c1[tid], v2 = c2[tid];
+        c1s[tid] = v1;
+        c2s[tid] = v2;
+    }
+    __syncthreads();
+
+    // one tile: x from buffer xb (its LDS-DMA retired by the counted wait)
+    auto compute_tile = [&](const float* __restrict__ xb, int tl) {
+        f32x4 acc[NT], cor[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = cor[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int p0 = 8 * s + 2 * kq;
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(xb + cl * KP + 4 * (p0 ^ (cl & SWM)));
+            const f32x4 hi =
+                *reinterpret_cast<const f32x4*>(xb + cl * KP + 4 * ((p0 + 1) ^ (cl & SWM)));
+            bf16x8 x1, x2, x3;
+            split3_x8(lo, hi, x1, x2, x3);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int o = (t * 16 + cl) * WSB + 32 * s + 8 * kq;
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&wsb[0][o]);
+                const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&wsb[1][o]);
+                const bf16x8 b3 = *reinterpret_cast<const bf16x8*>(&wsb[2][o]);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x1, acc[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, x1, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x2, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b3, x1, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, x2, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x3, cor[t], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[t][i] = split_sum(acc[t][i], cor[t][i]);
+        proj_direct_epilogue<NT>(acc, tl * 16 + cl, n, kq, bs, a1s, a2s, c1s, c2s, H, F, HF,
+                                 Wh, ld_wh, Ss, ld_s, s_dst, slice_w, slice_stride, store_wt);
+    };
+    // the ring, unrolled three ways so every buffer reference is static
+    auto step = [&](const float* cur, float* refill) -> bool {
+        if (tile >= tiles) return false;
+        fetch(tile + 2 * tstride, refill);
+        // this tile's DMAs retired; the next two tiles' (2 GLDS, issued later)
+        // may still fly.  Younger stores only make the wait longer.
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GLDS + EXTRA) : "memory");
+        compute_tile(cur, tile);
+        tile += tstride;
+        return true;
+    };
+    while (step(xr0[w], xr2[w]) && step(xr1[w], xr0[w]) && step(xr2[w], xr1[w])) {
+    }
+    // the prefetches past the last tile must land before the workgroup's LDS is
+    // released (an LDS-DMA into a freed allocation would corrupt the next one)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
 // Projection, whole-K variant (fin <= 64): the workgroup's 64 X rows are one
 // contiguous 64*fin*4-byte chunk of HBM, and W [HF, fin] is contiguous too, so
 // both are staged into LDS with fully coalesced float4 loads (16x fewer
@@ -1224,6 +1408,34 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         // over tiles): 3 per CU for K <= 64 (45 KB of LDS, <= 168 VGPRs), else 2
         int wg_cu = ks <= 2 ? 3 : 2;
         if (const char* v = knob("GAT_PROJ_WRES_WGS")) wg_cu = std::max(1, std::atoi(v));
+        // GAT_PROJ_WG (A/B knob): k_project_wg (x through LDS by LDS-DMA) for fin
+        // in {32, 64, 128} with 16-B aligned x and heads of 4, 8 or 16 columns;
+        // "2": the same with a store-aware DMA wait (vmcnt + 10, A/B only)
+        int wg = 0;
+        if (const char* v = knob("GAT_PROJ_WG")) wg = std::atoi(v);
+        const bool wg_ok = (fin == 32 || fin == 64 || fin == 128) &&
+                           ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15) == 0 &&
+                           (f == 4 || f == 8 || f == 16);
+        if (wg && wg_ok) {
+            const int grid_g = (int)std::max<long long>(1, std::min<long long>((tiles + 3) / 4, 256LL / ny));
+#define GAT_WG(NTV, KSV, EX)                                                                     \
+    hipLaunchKernelGGL((k_project_wg<NTV, KSV, EX>), dim3(grid_g, ny), dim3(256), 0, st, x, n, fin, \
+                       w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s,    \
+                       s_dst, slice_w, slice_stride, store_wt, crows, cjump)
+#define GAT_WG_KS(NTV, EX)                                  \
+    switch (ks) {                                           \
+        case 1: GAT_WG(NTV, 1, EX); break;                  \
+        case 2: GAT_WG(NTV, 2, EX); break;                  \
+        default: GAT_WG(NTV, 4, EX); break;                 \
+    }
+            if (wg == 2 && nt == 4) { GAT_WG_KS(4, 10) }
+            else if (nt == 1) { GAT_WG_KS(1, 0) }
+            else if (nt == 2) { GAT_WG_KS(2, 0) }
+            else { GAT_WG_KS(4, 0) }
+#undef GAT_WG_KS
+#undef GAT_WG
+            return status_of(hipGetLastError());
+        }
         const int grid_w = (int)std::max<long long>(
             1, std::min<long long>((tiles + 3) / 4, 256LL * wg_cu / ny));
 #define GAT_WRES(NTV, LWV, KSV)                                                               \

@@ -48,6 +48,8 @@ VARIANTS = {
     "proj_wres": {"GAT_PROJ_WRES": "1"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
     "proj_wk_lds_epilogue": {"GAT_PROJ_WK_DIRECT": "0"},
+    # k_project_wg: x through LDS by LDS-DMA (fin 32 / 64 / 128)
+    "proj_wg": {"GAT_PROJ_WG": "1"},
     "plain_stores": {"GAT_STORE_WT": "0"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
@@ -60,7 +62,7 @@ def variant(request, monkeypatch):
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
-              "GAT_EDGE_SPLIT"):
+              "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -132,6 +134,10 @@ CASES = [
     (333, 4000, 100, 8, 8, True, "uniform"),
     (50, 500, 66, 4, 4, False, "uniform"),
     (700, 9000, 0, 3, 4, True, "uniform"),  # Fin = 0: Wh = bias
+    # k_project_wg (fin 32 / 64 / 128): NT = 1, 2, 4; several ring turns per wave
+    (333, 4000, 32, 2, 8, False, "uniform"),
+    (1500, 20000, 64, 2, 16, True, "uniform"),
+    (60000, 200000, 128, 8, 8, True, "uniform"),
 ]
 
 
