@@ -188,6 +188,9 @@ def gat_layer_forward_rows(state: Dict[str, torch.Tensor], x: torch.Tensor,
         n = x.size(0)
         transformed, a1, a2 = _project_heads(x, *_state_params(state, num_heads))
         bias = state["bias"].detach().cpu()
+        # every sampled row's in-edges in one pass over edge_index (order kept),
+        # then each batch selects from that much smaller set
+        ei = ei[:, torch.isin(ei[1], rows)]
         outs = []
         for b0 in range(0, rows.numel(), batch):
             rb = rows[b0:b0 + batch]
