@@ -560,6 +560,7 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int cl = lane & 15, kq = lane >> 4;
     const int blk0 = blockIdx.x * BM;
+    if (blk0 >= n) return;  // a row chunk shorter than the grid (gat_project_chunked)
     const int row0 = blk0 + w * 16 * RG;  // wave w owns rows [16 RG w, 16 RG (w + 1))
     f32x4 acc[RG][NT], cor[RG][NT];
 #pragma unroll
@@ -1199,6 +1200,7 @@ __global__ __launch_bounds__(256) void k_project_wk(
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int cl = lane & 15, kq = lane >> 4;
     const int row0 = blockIdx.x * BM;
+    if (row0 >= n) return;  // a row chunk shorter than the grid (gat_project_chunked)
     const int rows = min(BM, n - row0);
     const int xs_n = round_up4(BM * fin);  // X tile floats (16-B aligned W tile after it)
     float* Xs = smem;
