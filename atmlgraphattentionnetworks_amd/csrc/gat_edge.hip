@@ -580,6 +580,155 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 }
 
 // ---------------------------------------------------------------------------
+// LDS-staged variant of k_edge_grp for short rows (north_star's "LDS staging of
+// neighbor Wh tiles per wavefront"; A/B knob GAT_EDGE_LDSDMA=1).  Same lane
+// groups (G lanes = one 128-B plane row or 256-B row, one float4 per lane,
+// U = 4 in-edges per chunk), but the source rows are not gathered into
+// registers: they arrive in a per-wave LDS ring by LDS-DMA
+// (global_load_lds_dwordx4, one wave-instruction per edge slot of the chunk:
+// lane l's 16 B of its row land at ring + 16 l), and so do the column
+// indices (global_load_lds_dword, G/U chunks per instruction).  With no VGPRs
+// held by loads in flight, every wave keeps D = 2 chunks of rows (and 3-5
+// chunks of indices) in flight while it scores and accumulates one chunk
+// read back from LDS.  The per-lane arithmetic is k_edge_grp's (fused source
+// score in log2 units, online softmax, concat + bias).  Eval only: no
+// dropout, no carried segment state, no Kahan rows (the launcher takes it
+// for short-row graphs only).  Ordering: every LDS read of a ring slot
+// follows a counted s_waitcnt vmcnt that retires that slot's DMAs (younger
+// DMAs may stay in flight); a slot is refilled one chunk after it was read.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* edge_lds_ptr;
+
+__device__ __forceinline__ void edge_dma16(const float* src, void* lds_dst) {
+    const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(edge_lds_ptr)lds_dst);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(l)
+        : "memory");
+}
+
+__device__ __forceinline__ void edge_dma4(const int* src, void* lds_dst) {
+    const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(edge_lds_ptr)lds_dst);
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(l)
+        : "memory");
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void k_edge_lds(
+    const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
+    int row_begin, int row_end, const float* __restrict__ Wh, int ld_wh,
+    const float* __restrict__ a_src, const float* __restrict__ c_src,
+    const float* __restrict__ s_dst, int H, int F, int HF, float slope,
+    const float* __restrict__ bias, float* __restrict__ out, int ld_out, int nslices,
+    int slice_w, long long slice_stride, int store_wt) {
+    constexpr int U = 4;
+    constexpr int CPD = G / U;        // chunks of indices per index DMA
+    constexpr int NB = 3;             // row ring: D = 2 chunks in flight + 1 read
+    constexpr int NC = 4;             // index ring (in index-DMA units)
+    __shared__ __attribute__((aligned(16))) float rowring[4][NB][U][kWave * 4];
+    __shared__ __attribute__((aligned(16))) int colring[4][NC][kWave];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & (G - 1), grp = lane / G;
+    const int sl = nslices > 1 ? (int)(blockIdx.x % (unsigned)nslices) : 0;
+    const unsigned blk = nslices > 1 ? blockIdx.x / (unsigned)nslices : blockIdx.x;
+    const int pos0 = row_begin + (int)((blk * (size_t)blockDim.x + threadIdx.x) / G);
+    const bool live = pos0 < row_end;
+    const int pos = live ? pos0 : row_end - 1;  // dead groups shadow a live row, store nothing
+    const int r = order != nullptr ? order[pos] : pos;
+    const int loff = 4 * c;                     // < slice width: G * 4 == row floats
+    const int coff = sl * slice_w + loff;
+    const float* __restrict__ Whs = Wh + (size_t)sl * (size_t)slice_stride + loff;
+    const int h = coff / F;
+    const f32x4 a4 = *reinterpret_cast<const f32x4*>(a_src + coff) * kLog2e;
+    const float c1 = c_src[h];
+    const int si = er.by_pos ? pos : r;
+    const int e0 = er.eb[si], e1 = er.ee[si];
+    const int len = e1 - e0;
+    const float sd = (s_dst[(size_t)r * H + h] + c1) * kLog2e;
+    // chunks this wave walks: the longest of its rows (rows are degree-ordered)
+    int nch = (len + U - 1) / U;
+#pragma unroll
+    for (int off = G; off < kWave; off <<= 1) nch = max(nch, __shfl_xor(nch, off));
+    const int elast = e1 > e0 ? e1 - 1 : (e0 > 0 ? e0 - 1 : 0);  // a valid index position
+    // index DMA for index block q (chunks q*CPD .. q*CPD+CPD-1 of every row)
+    auto fetch_cols = [&](int q) {
+        const int e = min(e0 + (q * CPD + c / U) * U + (c % U), elast);
+        edge_dma4(col + e, &colring[w][q % NC][0]);
+    };
+    // row DMAs of chunk k: slot u for all groups of the wave
+    auto fetch_rows = [&](int k) {
+        const int* cw = &colring[w][(k / CPD) % NC][grp * G + (k % CPD) * U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) edge_dma16(Whs + (size_t)cw[u] * ld_wh, &rowring[w][k % NB][u][0]);
+    };
+    // prologue: indices of chunks 0 .. 3*CPD-1, then rows of chunks 0 and 1
+    fetch_cols(0);
+    fetch_cols(1);
+    fetch_cols(2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fetch_rows(0);
+    fetch_rows(1);
+    float m = -INFINITY, l = 0.f;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < nch; ++k) {
+        // indices CPD*3 chunks ahead (their DMA retires behind the row DMAs the
+        // waits below retire); rows 2 chunks ahead
+        if (k % CPD == 0) fetch_cols(k / CPD + 3);
+        fetch_rows(k + 2);  // past the row end: clamped indices, unused
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * U) : "memory");
+        const int nk = min(U, e1 - (e0 + k * U));
+        if (nk > 0) {
+            f32x4 v[U];
+            float sc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                v[u] = *reinterpret_cast<const f32x4*>(&rowring[w][k % NB][u][4 * lane]);
+                f32x2 d2 = f32x2{v[u].x, v[u].y} * f32x2{a4.x, a4.y};
+                d2 += f32x2{v[u].z, v[u].w} * f32x2{a4.z, a4.w};
+                sc[u] = d2.x + d2.y;
+            }
+            const int hl = F / 4;
+            if (hl > 1) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) sc[u] = group_sum16(sc[u], hl);
+            }
+            float emax = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float z = sd + sc[u];
+                sc[u] = u < nk ? fmaxf(z, z * slope) : -INFINITY;
+                emax = fmaxf(emax, sc[u]);
+            }
+            const float m_new = fmaxf(m, emax);
+            const float scale = __builtin_amdgcn_exp2f(m - m_new);
+            l *= scale;
+            acc *= scale;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const float p = __builtin_amdgcn_exp2f(sc[u] - m_new);
+                l += p;
+                acc += p * v[u];
+            }
+            m = m_new;
+        }
+    }
+    // the row DMAs issued past the last chunk must land before the LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!live) return;
+    const float inv = 1.f / (l + 1e-16f);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(bias + coff);
+    store_out4(out, (size_t)r * ld_out + coff, acc * inv + b, store_wt);
+}
+
+// ---------------------------------------------------------------------------
 // Merge of split hub rows (degree skew).  A target row with more in-edges
 // than one lane group should walk serially is cut into segments that run as
 // separate virtual rows of k_edge_grp (EdgeRows by_pos + store), in parallel;
@@ -786,6 +935,26 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // waves per SIMD (PPI at P = 8: 9.0 -> 8.2 us; at P = 4 it is 13.6).
         // Rows of fewer than ~3 chunks per group gain nothing from a split (arxiv
         // at P = 8, 8 edges per row: 10.9 us whole, 12.0 / 15.8 split 2 / 4).
+        // GAT_EDGE_LDSDMA=1 (A/B knob): the LDS-staged short-row kernel
+        // (k_edge_lds) where it applies: eval, concat, fused score, U = 4,
+        // one float4 per lane, a lane group = one 128-B plane row or 256-B row
+        if (const char* ld = knob("GAT_EDGE_LDSDMA")) {
+            if (std::atoi(ld) == 1 && fused && vv == 1 && u == 4 && !kink && concat &&
+                !er.load && er.store_lt == 0 && drop.thresh == 0 && lse == nullptr &&
+                y_heads == nullptr && (g == 8 || g == 16) && 4 * g == gcols) {
+                if (g == 8)
+                    hipLaunchKernelGGL((k_edge_lds<8>), grid, block, 0, st, er, col, row_order,
+                                       row_begin, row_end, wh, ld_wh, a_src, c_src, s_dst, heads,
+                                       f, hf, negative_slope, bias, out, ld_out, nslices, slice_w,
+                                       slice_stride, store_wt);
+                else
+                    hipLaunchKernelGGL((k_edge_lds<16>), grid, block, 0, st, er, col, row_order,
+                                       row_begin, row_end, wh, ld_wh, a_src, c_src, s_dst, heads,
+                                       f, hf, negative_slope, bias, out, ld_out, nslices, slice_w,
+                                       slice_stride, store_wt);
+                return status_of(hipGetLastError());
+            }
+        }
         const long long waves = (long long)rows * g * nslices / kWave;
         const int chunks = edges_per_row_hint > 0 ? edges_per_row_hint / u : 1 << 20;
         int split = (waves < 2048 && chunks >= 6) ? 4 : (waves < 4096 && chunks >= 3) ? 2 : 1;

@@ -53,6 +53,8 @@ VARIANTS = {
     "plain_stores": {"GAT_STORE_WT": "0"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
+    # the LDS-staged short-row edge kernel (k_edge_lds, A/B): rows by LDS-DMA
+    "edge_lds": {"GAT_EDGE_LDSDMA": "1"},
 }
 
 
@@ -62,7 +64,7 @@ def variant(request, monkeypatch):
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
-              "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V"):
+              "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)

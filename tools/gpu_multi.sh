@@ -34,6 +34,16 @@ for STEP in "$@"; do
       W=${ARG%%|*}; V=${ARG#*|}
       timeout -k 10 600 python3 -u tools/edge_ab.py --workload $W --variants "$V" > $OUT.json 2> $OUT.err || { echo "FAILED"; tail -20 $OUT.err; exit 1; }
       cat $OUT.json ;;
+    sq)
+      # SQ / TCP counters of the projection at one shape under one variant
+      S=${ARG%%|*}; V=${ARG#*|}
+      j=0
+      for CTRS in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM SQ_VALU_MFMA_BUSY_CYCLES" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE" "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+        j=$((j+1))
+        timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d ${OUT}_p$j -o run -- python3 tools/proj_bench.py --shapes "$S" --variants "$V" --rounds 1 --iters 4 > ${OUT}_p$j.log 2>&1 || { echo "FAILED pass $j"; tail -5 ${OUT}_p$j.log; exit 1; }
+      done
+      python3 tools/sq_summary.py ${OUT}_p* > $OUT.txt 2>&1
+      cat $OUT.txt ;;
     *) echo "unknown step $KIND"; exit 2 ;;
   esac
 done
