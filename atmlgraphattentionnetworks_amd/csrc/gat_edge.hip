@@ -919,7 +919,13 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // wave per SIMD at 360 registers, but 64 row gathers in flight per
         // lane; tools/slice_probe.py, Reddit scale 2.60 -> 1.99 ms); shorter
         // rows keep more, shallower waves (PPI 30.5 -> 32.9 us pipelined)
-        int pipe = (u == 16 && vv == 2) ? 1 : 0;
+        // Not for the multi-GPU segment passes (rows' edges split over the
+        // all-gather chunks, the state carried between passes): there the
+        // one-wave-per-SIMD pipelined kernel exposes each pass's row prologue
+        // (Reddit at P = 8, 3 passes: 342 us pipelined vs 287 us not; one
+        // unsplit pass 252 vs 292; tools/emu_probe.py, profiles/r04/emu_reddit_p8.json)
+        const bool seg_pass = !er.by_pos && (er.load || er.store_lt > 0);
+        int pipe = (u == 16 && vv == 2 && !seg_pass) ? 1 : 0;
         if (const char* ep = knob("GAT_EDGE_PIPE")) pipe = std::atoi(ep);
         // two lane groups per row (the grid doubles inside launch_edge_fused):
         // GAT_EDGE_SPLIT = 2 (A/B knob); the kink-sum forward and the pipelined

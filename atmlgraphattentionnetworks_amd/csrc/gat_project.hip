@@ -971,31 +971,34 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
 }
 
 // ---------------------------------------------------------------------------
-// Projection for fin in {32, 64, 128} (ogbn-arxiv's 128): k_project_wres's
-// W-resident split-bf16 form, with x streamed through LDS by LDS-DMA
-// (global_load_lds_dwordx4) instead of fragment-shaped loads into registers.
+// Projection for fin in {32, 64, 128} (ogbn-arxiv's 128), split-bf16 MFMA:
+// W held in REGISTERS, x streamed through LDS by LDS-DMA.
 //
-// A 16-row x tile is one contiguous 16*fin*4-byte run (x 16-B aligned), so
-// each wave fetches its tiles in whole 1-KiB wave-instructions (8 per tile at
-// fin = 128), fully coalesced, into a private ring of NB = 3 tile buffers:
-// tiles i+1 and i+2 are in flight while tile i is computed, with no VGPRs
-// spent on them and no per-element address arithmetic (fragment-shaped loads
-// touch 16 rows x 32 B per instruction: MI355X_MICROARCH / cdna guide measure
-// them at ~2x the TA time of full-line staging).  The LDS image is
-// XOR-swizzled through the SOURCE address (LDS-DMA writes lane-linear): 16-B
-// piece p of row r lands at p ^ (r & 15), so the A/B fragment reads
-// (ds_read_b128, rows cl = 0..15) hit 16 distinct 4-bank groups.
-// Operands swapped as k_project_wk's DIRECT form (A = W fragment, B = x
-// fragment): each lane ends with four consecutive Wh columns of one row and
-// the epilogue stores them straight from registers (proj_direct_epilogue).
-// Ordering: a wave reads only buffers it filled itself, after a counted
-// s_waitcnt vmcnt that retires that tile's LDS-DMA (the two younger tiles'
-// 2 * GLDS DMAs, and any younger stores, may stay in flight); a buffer is
-// refilled one iteration after its fragments were consumed by MFMAs.
-// One workgroup per CU (W planes 52 KB + 4 waves x 3 x 8 KB ring).
+// With K <= 128 and <= 64 columns, a lane's W fragments for every k-step and
+// column tile (split into three bf16 terms once, as k_project_x3 splits W)
+// are <= 16 x 3 bf16x8 = 192 VGPRs: each wave loads and splits them once and
+// then loops over 16-row x tiles with no W traffic at all (k_project_wres
+// re-reads 48 W fragments per tile from LDS).  A 16-row x tile is one
+// contiguous 16*fin*4-byte run (x 16-B aligned), fetched in whole 1-KiB
+// wave-instructions (global_load_lds_dwordx4, 8 per tile at fin = 128) into a
+// private ring of 4 LDS tile buffers: 3 tiles in flight while one is computed,
+// no VGPRs held by them and no per-element address arithmetic (fragment-shaped
+// loads touch 16 rows x 32 B per instruction).  The LDS image is XOR-swizzled
+// through the SOURCE address (LDS-DMA writes lane-linear): 16-B piece p of row
+// r lands at p ^ (r & 15), so the fragment reads (ds_read_b128, rows 0..15)
+// hit 16 distinct 4-bank groups.  Operands swapped as k_project_wk's DIRECT
+// form (A = W fragment, B = x fragment): each lane ends with four consecutive
+// Wh columns of one row, stored straight from registers (proj_direct_epilogue).
+// Ordering: a wave reads only ring buffers it filled, after a counted
+// s_waitcnt vmcnt that retires that tile's DMAs (the three younger tiles'
+// 3 * GLDS DMAs, and any younger stores, may stay in flight); a buffer is
+// refilled one tile after its fragments were read.  The DMAs are issued by
+// inline asm so that the compiler, which cannot see them, never adds a
+// conservative vmcnt(0) before the ring reads; its own waits for its own
+// loads can only be longer than needed, never shorter.
+// One workgroup of 4 waves per CU (one wave per SIMD: ~300 VGPRs).
 // ---------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
-typedef __attribute__((address_space(1))) void* gbl_void_ptr;
 
 template <int NT, int KS, int EXTRA = 0>
 __global__ __launch_bounds__(256, 1) void k_project_wg(
@@ -1008,19 +1011,16 @@ __global__ __launch_bounds__(256, 1) void k_project_wg(
     long long cjump) {
     GAT_ROW_CHUNKS();
     constexpr int BN = NT * 16, KP = KS * 32;  // fin == KP
-    constexpr int WSB = KP + 8;
     constexpr int TILE = 16 * KP;              // floats per x tile
     constexpr int PIECES = KP / 4;             // 16-B pieces per x row (8, 16 or 32)
     constexpr int SWM = PIECES < 16 ? PIECES - 1 : 15;
     constexpr int GLDS = TILE / 256;           // 1-KiB LDS-DMA wave-instructions per tile
     static_assert(GLDS >= 1 && (PIECES & (PIECES - 1)) == 0, "fin must be 32, 64 or 128");
-    __shared__ __attribute__((aligned(16))) __bf16 wsb[3][BN * WSB];
-    // three separate ring buffers (not one indexed array): the compiler's
-    // waitcnt pass then sees that a fragment read of one buffer cannot alias
-    // the LDS-DMA in flight into the others, and does not wait vmcnt(0)
+    // four separate ring buffers (static references only)
     __shared__ __attribute__((aligned(16))) float xr0[4][TILE];
     __shared__ __attribute__((aligned(16))) float xr1[4][TILE];
     __shared__ __attribute__((aligned(16))) float xr2[4][TILE];
+    __shared__ __attribute__((aligned(16))) float xr3[4][TILE];
     __shared__ __attribute__((aligned(16))) float prm[3 * BN + 2 * 64];
     float* bs = prm;
     float* a1s = prm + BN;
@@ -1033,20 +1033,22 @@ __global__ __launch_bounds__(256, 1) void k_project_wg(
     const int tiles = (n + 15) / 16;
     const int tstride = gridDim.x * 4;
     int tile = blockIdx.x * 4 + w;
-    // LDS-DMA of one tile into ring buffer b: unit u = 64 i + lane of the tile
-    // image holds row u / PIECES, stored piece u % PIECES = source piece ^ swizzle
+    // this lane's source offsets inside a tile: DMA unit u = 64 i + lane holds
+    // row u / PIECES, stored piece u % PIECES = source piece ^ swizzle
+    int soff[GLDS], srow[GLDS];
+#pragma unroll
+    for (int i = 0; i < GLDS; ++i) {
+        const int u = i * 64 + lane;
+        srow[i] = u / PIECES;
+        soff[i] = 4 * ((u % PIECES) ^ (srow[i] & SWM));
+    }
     auto fetch = [&](int tl, float* dst) {
         const int t = min(tl, tiles - 1);  // past the end: a harmless reload
+        const bool full = t * 16 + 16 <= n;  // wave-uniform
 #pragma unroll
         for (int i = 0; i < GLDS; ++i) {
-            const int u = i * 64 + lane;
-            const int r = u / PIECES, pc = u % PIECES;
-            const int grow = min(t * 16 + r, n - 1);
-            const float* src = X + (size_t)grow * KP + 4 * (pc ^ (r & SWM));
-            // by inline asm: the compiler then does not track these DMAs, so it
-            // never adds its own conservative vmcnt(0) before the ring's fragment
-            // reads (its waits for its own loads can only grow longer, never
-            // shorter); the counted waits below order the reads
+            const int grow = full ? t * 16 + srow[i] : min(t * 16 + srow[i], n - 1);
+            const float* src = X + (size_t)grow * KP + soff[i];
             const unsigned ldst = __builtin_amdgcn_readfirstlane(
                 (unsigned)(uintptr_t)(lds_void_ptr)(dst + i * 256));  // wave-uniform
             unsigned keep;
@@ -1060,31 +1062,19 @@ __global__ __launch_bounds__(256, 1) void k_project_wg(
     };
     fetch(tile, xr0[w]);
     fetch(tile + tstride, xr1[w]);
-    // W split into three bf16 planes (k_project_wres's loads: unconditional,
-    // clamped, all issued together), zero past HF columns
-    {
-        constexpr int WQ = (BN * KP + 256 * 4 - 1) / (256 * 4);
-        f32x4 wv[WQ];
+    fetch(tile + 2 * tstride, xr2[w]);
+    // this lane's W fragments, split into three bf16 terms (zero past HF)
+    bf16x8 wf1[KS][NT], wf2[KS][NT], wf3[KS][NT];
 #pragma unroll
-        for (int q = 0; q < WQ; ++q) {
-            const int e = (tid + 256 * q) * 4;
-            const int c = min(e / KP, HF - 1), k = e % KP;
-            wv[q] = *reinterpret_cast<const f32x4*>(W + (size_t)c * KP + k);
-        }
+    for (int t = 0; t < NT; ++t) {
+        const int cc = t * 16 + cl;
+        const float* wr = W + (size_t)min(cc, HF - 1) * KP + 8 * kq;
 #pragma unroll
-        for (int q = 0; q < WQ; ++q) {
-            const int e = (tid + 256 * q) * 4;
-            if (e < BN * KP) {
-                const int c = e / KP, k = e % KP;
-                const f32x4 v = c < HF ? wv[q] : f32x4{0.f, 0.f, 0.f, 0.f};
-                bf16x2 p1a, p2a, p3a, p1b, p2b, p3b;
-                split3_pair(f32x2{v.x, v.y}, p1a, p2a, p3a);
-                split3_pair(f32x2{v.z, v.w}, p1b, p2b, p3b);
-                const int o = c * WSB + k;
-                *reinterpret_cast<bf16x4*>(&wsb[0][o]) = bf16x4{p1a[0], p1a[1], p1b[0], p1b[1]};
-                *reinterpret_cast<bf16x4*>(&wsb[1][o]) = bf16x4{p2a[0], p2a[1], p2b[0], p2b[1]};
-                *reinterpret_cast<bf16x4*>(&wsb[2][o]) = bf16x4{p3a[0], p3a[1], p3b[0], p3b[1]};
-            }
+        for (int s2 = 0; s2 < KS; ++s2) {
+            f32x4 lo = *reinterpret_cast<const f32x4*>(wr + 32 * s2);
+            f32x4 hi = *reinterpret_cast<const f32x4*>(wr + 32 * s2 + 4);
+            if (cc >= HF) lo = hi = f32x4{0.f, 0.f, 0.f, 0.f};
+            split3_x8(lo, hi, wf1[s2][t], wf2[s2][t], wf3[s2][t]);
         }
     }
     if (tid < BN) {
@@ -1102,14 +1092,13 @@ __global__ __launch_bounds__(256, 1) void k_project_wg(
     }
     __syncthreads();
 
-    // one tile: x from buffer xb (its LDS-DMA retired by the counted wait)
     auto compute_tile = [&](const float* __restrict__ xb, int tl) {
         f32x4 acc[NT], cor[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[t] = cor[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const int p0 = 8 * s + 2 * kq;
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const int p0 = 8 * s2 + 2 * kq;
             const f32x4 lo = *reinterpret_cast<const f32x4*>(xb + cl * KP + 4 * (p0 ^ (cl & SWM)));
             const f32x4 hi =
                 *reinterpret_cast<const f32x4*>(xb + cl * KP + 4 * ((p0 + 1) ^ (cl & SWM)));
@@ -1117,16 +1106,12 @@ __global__ __launch_bounds__(256, 1) void k_project_wg(
             split3_x8(lo, hi, x1, x2, x3);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                const int o = (t * 16 + cl) * WSB + 32 * s + 8 * kq;
-                const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&wsb[0][o]);
-                const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&wsb[1][o]);
-                const bf16x8 b3 = *reinterpret_cast<const bf16x8*>(&wsb[2][o]);
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x1, acc[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, x1, cor[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x2, cor[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b3, x1, cor[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, x2, cor[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x3, cor[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[s2][t], x1, acc[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf2[s2][t], x1, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[s2][t], x2, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf3[s2][t], x1, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf2[s2][t], x2, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[s2][t], x3, cor[t], 0, 0, 0);
             }
         }
 #pragma unroll
@@ -1136,18 +1121,19 @@ __global__ __launch_bounds__(256, 1) void k_project_wg(
         proj_direct_epilogue<NT>(acc, tl * 16 + cl, n, kq, bs, a1s, a2s, c1s, c2s, H, F, HF,
                                  Wh, ld_wh, Ss, ld_s, s_dst, slice_w, slice_stride, store_wt);
     };
-    // the ring, unrolled three ways so every buffer reference is static
+    // the ring, unrolled four ways so every buffer reference is static
     auto step = [&](const float* cur, float* refill) -> bool {
         if (tile >= tiles) return false;
-        fetch(tile + 2 * tstride, refill);
-        // this tile's DMAs retired; the next two tiles' (2 GLDS, issued later)
-        // may still fly.  Younger stores only make the wait longer.
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GLDS + EXTRA) : "memory");
+        fetch(tile + 3 * tstride, refill);
+        // this tile's DMAs retired; the next three tiles' (3 GLDS, issued
+        // later) may still fly.  Younger stores only make the wait longer.
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GLDS + EXTRA) : "memory");
         compute_tile(cur, tile);
         tile += tstride;
         return true;
     };
-    while (step(xr0[w], xr2[w]) && step(xr1[w], xr0[w]) && step(xr2[w], xr1[w])) {
+    while (step(xr0[w], xr3[w]) && step(xr1[w], xr0[w]) && step(xr2[w], xr1[w]) &&
+           step(xr3[w], xr2[w])) {
     }
     // the prefetches past the last tile must land before the workgroup's LDS is
     // released (an LDS-DMA into a freed allocation would corrupt the next one)
@@ -1521,8 +1507,13 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         // "b64p1": 64 rows, one chunk in flight; "b64p1w3": the same bounded to 3
         // workgroups per CU; "b128w2": 128 rows bounded to 2 workgroups per CU
         // (k_project_x3<.., 2, 1> unbounded takes 308 registers: one wave per SIMD)
-        int x3v = 0;
+        // default for 8-B aligned rows (Reddit's 602): 64-row blocks, one chunk in
+        // flight (188 registers, 2 waves per SIMD; tools/proj_bench.py: full
+        // Reddit 204 -> 201 us, a P = 8 rank's 29k rows 34.4 -> 29.1 us: twice
+        // the blocks fill the CUs; profiles/r04/proj_x3v.json)
+        int x3v = lw == 2 ? 1 : 0;
         if (const char* v = knob("GAT_PROJ_X3V")) {
+            x3v = 0;
             if (std::strcmp(v, "b64p1") == 0) x3v = 1;
             else if (std::strcmp(v, "b64p1w3") == 0) x3v = 2;
             else if (std::strcmp(v, "b128w2") == 0) x3v = 3;

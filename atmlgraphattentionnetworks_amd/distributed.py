@@ -144,14 +144,17 @@ EDGES_PER_CHUNK = 4_000_000  # per-rank edges per all-gather chunk / edge pass
 
 def default_chunks(world: int, total_edges: int, fused: bool) -> int:
     """All-gather chunks (= edge passes) per step: one pass per ~4M edges per
-    rank, at most 4; 1 on a single rank or without the fused kernels.
+    rank, at most 2 (each extra pass re-runs every row's prologue and carries
+    its state through memory: Reddit at P = 8, edge passes 279 / 287 us at 2 / 3
+    chunks, P = 4 555 us at 4; profiles/r04/emu_reddit_p8.json); 1 on a single
+    rank or without the fused kernels.
 
     Every rank must pick the SAME count (it fixes the table layout and the
     collectives' sizes), so the argument is the graph's total edge count E',
     which all ranks see, never a rank's own share."""
     if world <= 1 or not fused:
         return 1
-    return max(1, min(4, (total_edges // world) // EDGES_PER_CHUNK))
+    return max(1, min(2, (total_edges // world) // EDGES_PER_CHUNK))
 
 
 class HipOps:
