@@ -571,7 +571,9 @@ def emulated_ranks(meas: dict, ranks, exchanges=("allgather",)) -> dict:
         for exch in exchanges:
             for p in ranks:
                 _log(f"{meas['workload']}: emulated P={p} ({exch})")
-                r = emulate_rank_times(layer, csr, x, p, exchange=exch)
+                # "allgather_k1": one unsplit edge pass (the compute floor, no overlap)
+                kind, chunks = ("allgather", 1) if exch == "allgather_k1" else (exch, None)
+                r = emulate_rank_times(layer, csr, x, p, exchange=kind, chunks=chunks)
                 r["compute_only_speedup_bound"] = meas["ms_per_step"] / r["max_compute_ms"]
                 r["per_rank"] = [{k: (round(v, 5) if isinstance(v, float) else v)
                                   for k, v in d.items()} for d in r["per_rank"]]
@@ -657,6 +659,9 @@ def main():
         if emu_ranks and nm in ("arxiv", "reddit"):
             emulated[nm] = emulated_ranks(m, emu_ranks, ("allgather", "replicate")
                                           if nm == "arxiv" else ("allgather",))
+            if nm == "reddit" and 8 in emu_ranks:
+                # the same step with one unsplit edge pass (no all-gather overlap)
+                emulated[nm].update(emulated_ranks(m, [8], ("allgather_k1",)))
         if nm == "reddit" and not args.no_train:
             # the training step against the eval forward
             xw, eiw, lw = m["_inputs"]

@@ -44,6 +44,18 @@ for STEP in "$@"; do
       done
       python3 tools/sq_summary.py ${OUT}_p* > $OUT.txt 2>&1
       cat $OUT.txt ;;
+    edgepmc)
+      # edge A/B, then per variant: fabric reads + L2 hit, and SQ wait/active counters
+      W=${ARG%%|*}; V=${ARG#*|}
+      timeout -k 10 600 python3 -u tools/edge_ab.py --workload $W --rounds 5 --variants "$V" > $OUT.json 2> $OUT.err || { echo "FAILED"; tail -20 $OUT.err; exit 1; }
+      cat $OUT.json
+      IFS=';' read -ra VV <<< "$V"
+      for vi in "${!VV[@]}"; do
+        timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_128B_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d ${OUT}_pmc_v$vi -o run -- python3 tools/edge_ab.py --workload $W --variants "$V" --only $vi --iters 3 > ${OUT}_pmc_v$vi.log 2>&1 || { echo "FAILED pmc $vi"; exit 1; }
+        timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --output-format csv -d ${OUT}_sq_v$vi -o run -- python3 tools/edge_ab.py --workload $W --variants "$V" --only $vi --iters 3 > ${OUT}_sq_v$vi.log 2>&1 || { echo "FAILED sq $vi"; exit 1; }
+      done
+      python3 tools/pmc_edge_summary.py ${OUT}_pmc_v* > $OUT.pmc.json 2>&1; cat $OUT.pmc.json
+      python3 tools/sq_summary.py ${OUT}_sq_v* > $OUT.sq.txt 2>&1; cat $OUT.sq.txt ;;
     *) echo "unknown step $KIND"; exit 2 ;;
   esac
 done
