@@ -36,6 +36,7 @@ from __future__ import annotations
 
 import json
 import os
+import statistics
 import sys
 import time
 from dataclasses import dataclass
@@ -533,8 +534,10 @@ def emulate_rank_times(layer, csr, x, world: int, exchange: str = "allgather",
     ranks, xs = _emulated_ranks(layer, csr, x, world, exchange, chunks)
     per = []
     for sh, xl in zip(ranks, xs):
-        proj = _event_ms(lambda: sh.phase_project(xl), iters)
-        edge = _event_ms(sh.phase_edges, iters)
+        # median of 3 measurements of `iters` launches each: one rank's single
+        # disturbed measurement would otherwise set the max over ranks
+        proj = statistics.median(_event_ms(lambda: sh.phase_project(xl), iters) for _ in range(3))
+        edge = statistics.median(_event_ms(sh.phase_edges, iters) for _ in range(3))
         per.append({"rank": sh.rank, "rows": sh.n_local, "local_edges": sh.local.num_edges,
                     "project_ms": proj, "edge_passes_ms": edge})
     lay = ranks[0].layout

@@ -56,6 +56,16 @@ for STEP in "$@"; do
       done
       python3 tools/pmc_edge_summary.py ${OUT}_pmc_v* > $OUT.pmc.json 2>&1; cat $OUT.pmc.json
       python3 tools/sq_summary.py ${OUT}_sq_v* > $OUT.sq.txt 2>&1; cat $OUT.sq.txt ;;
+    trainsq)
+      # SQ / TCP / TCC counters over a training step (tools/train_probe.py)
+      W=${ARG%%|*}; N=${ARG#*|}
+      j=0
+      for CTRS in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_INST_LEVEL_VMEM GRBM_GUI_ACTIVE" "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE" "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" "TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum GRBM_GUI_ACTIVE"; do
+        j=$((j+1))
+        timeout -s KILL 300 rocprofv3 --pmc $CTRS --output-format csv -d ${OUT}_p$j -o run -- python3 tools/train_probe.py $W $N > ${OUT}_p$j.log 2>&1 || { echo "FAILED pass $j"; tail -5 ${OUT}_p$j.log; exit 1; }
+      done
+      python3 tools/sq_summary.py ${OUT}_p* > $OUT.txt 2>&1
+      cat $OUT.txt ;;
     *) echo "unknown step $KIND"; exit 2 ;;
   esac
 done

@@ -14,7 +14,7 @@ for d in sys.argv[1:]:
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
             n = r["Kernel_Name"]
-            if "k_edge" not in n and "k_project" not in n:
+            if not any(k in n for k in ("k_edge", "k_project", "k_bwd", "k_wgrad", "k_dx")):
                 continue
             key = short_name(n)
             per.setdefault(key, {}).setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
