@@ -579,6 +579,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     }
 }
 
+#ifdef GAT_AB_KERNELS  // measured and not adopted (profiles/r04/edge_ab_lds_*.json); tools-only build
 // ---------------------------------------------------------------------------
 // LDS-staged variant of k_edge_grp for short rows (north_star's "LDS staging of
 // neighbor Wh tiles per wavefront"; A/B knob GAT_EDGE_LDSDMA=1).  Same lane
@@ -727,6 +728,8 @@ __global__ __launch_bounds__(256) void k_edge_lds(
     const f32x4 b = *reinterpret_cast<const f32x4*>(bias + coff);
     store_out4(out, (size_t)r * ld_out + coff, acc * inv + b, store_wt);
 }
+
+#endif  // GAT_AB_KERNELS
 
 // ---------------------------------------------------------------------------
 // Merge of split hub rows (degree skew).  A target row with more in-edges
@@ -941,6 +944,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // waves per SIMD (PPI at P = 8: 9.0 -> 8.2 us; at P = 4 it is 13.6).
         // Rows of fewer than ~3 chunks per group gain nothing from a split (arxiv
         // at P = 8, 8 edges per row: 10.9 us whole, 12.0 / 15.8 split 2 / 4).
+#ifdef GAT_AB_KERNELS
         // GAT_EDGE_LDSDMA=1 (A/B knob): the LDS-staged short-row kernel
         // (k_edge_lds) where it applies: eval, concat, fused score, U = 4,
         // one float4 per lane, a lane group = one 128-B plane row or 256-B row
@@ -961,6 +965,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
                 return status_of(hipGetLastError());
             }
         }
+#endif
         const long long waves = (long long)rows * g * nslices / kWave;
         const int chunks = edges_per_row_hint > 0 ? edges_per_row_hint / u : 1 << 20;
         int split = (waves < 2048 && chunks >= 6) ? 4 : (waves < 4096 && chunks >= 3) ? 2 : 1;

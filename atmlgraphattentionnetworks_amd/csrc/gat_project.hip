@@ -970,6 +970,7 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
     }
 }
 
+#ifdef GAT_AB_KERNELS  // measured and not adopted (profiles/r04/proj_ab.json); tools-only build
 // ---------------------------------------------------------------------------
 // Projection for fin in {32, 64, 128} (ogbn-arxiv's 128), split-bf16 MFMA:
 // W held in REGISTERS, x streamed through LDS by LDS-DMA.
@@ -1139,6 +1140,8 @@ __global__ __launch_bounds__(256, 1) void k_project_wg(
     // released (an LDS-DMA into a freed allocation would corrupt the next one)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+
+#endif  // GAT_AB_KERNELS
 
 // ---------------------------------------------------------------------------
 // Projection, whole-K variant (fin <= 64): the workgroup's 64 X rows are one
@@ -1396,6 +1399,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         // over tiles): 3 per CU for K <= 64 (45 KB of LDS, <= 168 VGPRs), else 2
         int wg_cu = ks <= 2 ? 3 : 2;
         if (const char* v = knob("GAT_PROJ_WRES_WGS")) wg_cu = std::max(1, std::atoi(v));
+#ifdef GAT_AB_KERNELS
         // GAT_PROJ_WG (A/B knob): k_project_wg (x through LDS by LDS-DMA) for fin
         // in {32, 64, 128} with 16-B aligned x and heads of 4, 8 or 16 columns;
         // "2": the same with a store-aware DMA wait (vmcnt + 10, A/B only)
@@ -1424,6 +1428,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #undef GAT_WG
             return status_of(hipGetLastError());
         }
+#endif
         const int grid_w = (int)std::max<long long>(
             1, std::min<long long>((tiles + 3) / 4, 256LL * wg_cu / ny));
 #define GAT_WRES(NTV, LWV, KSV)                                                               \

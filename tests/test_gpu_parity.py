@@ -48,13 +48,9 @@ VARIANTS = {
     "proj_wres": {"GAT_PROJ_WRES": "1"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
     "proj_wk_lds_epilogue": {"GAT_PROJ_WK_DIRECT": "0"},
-    # k_project_wg: x through LDS by LDS-DMA (fin 32 / 64 / 128)
-    "proj_wg": {"GAT_PROJ_WG": "1"},
     "plain_stores": {"GAT_STORE_WT": "0"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
-    # the LDS-staged short-row edge kernel (k_edge_lds, A/B): rows by LDS-DMA
-    "edge_lds": {"GAT_EDGE_LDSDMA": "1"},
 }
 
 
@@ -136,7 +132,8 @@ CASES = [
     (333, 4000, 100, 8, 8, True, "uniform"),
     (50, 500, 66, 4, 4, False, "uniform"),
     (700, 9000, 0, 3, 4, True, "uniform"),  # Fin = 0: Wh = bias
-    # k_project_wg (fin 32 / 64 / 128): NT = 1, 2, 4; several ring turns per wave
+    # fin 32 / 64 / 128 with NT = 1, 2, 4 and many tiles per wave (k_project_wres,
+    # k_project_wg in the tools-only GAT_AB_KERNELS build)
     (333, 4000, 32, 2, 8, False, "uniform"),
     (1500, 20000, 64, 2, 16, True, "uniform"),
     (60000, 200000, 128, 8, 8, True, "uniform"),
