@@ -47,7 +47,7 @@ const char* knob(const char* name) {
 
 int store_wt_on() {
     const char* v = knob("GAT_STORE_WT");
-    return v != nullptr ? (std::atoi(v) != 0) : 1;
+    return v != nullptr ? std::max(0, std::min(3, std::atoi(v))) : 1;
 }
 
 bool kernel_choice(const char* env, const char* slow) {

@@ -213,11 +213,19 @@ __device__ __forceinline__ float group_sum16(float v, int w) {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr size_t kWtMaxOff = 0x7FFFFFF0u;
 
+// wt: 0 plain store; 1 write-through (sc1, the default); 2 non-temporal (nt,
+// streamed past the caches); 3 nt + sc1 (GAT_STORE_WT A/B knob values)
 __device__ __forceinline__ void store_out4(float* base, size_t idx, f32x4 v, int wt) {
     const size_t off = idx * sizeof(float);
     if (wt && off < kWtMaxOff) {
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, (int)off, 0, 16);
+        const u32x4 bits = __builtin_bit_cast(u32x4, v);
+        if (wt == 2)
+            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (int)off, 0, 2);
+        else if (wt == 3)
+            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (int)off, 0, 18);
+        else
+            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (int)off, 0, 16);
     } else {
         *reinterpret_cast<f32x4*>(base + idx) = v;
     }
@@ -227,7 +235,12 @@ __device__ __forceinline__ void store_out1(float* base, size_t idx, float v, int
     const size_t off = idx * sizeof(float);
     if (wt && off < kWtMaxOff) {
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 16);
+        if (wt == 2)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 2);
+        else if (wt == 3)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 18);
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 16);
     } else {
         base[idx] = v;
     }
