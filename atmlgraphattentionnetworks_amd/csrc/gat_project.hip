@@ -571,38 +571,53 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
     // PD chunks of loads in flight (PD = 2: a register double buffer,
     // statically indexed)
     vec xa_[XL], wa_[WL], xb_[PD == 2 ? XL : 1], wb_[PD == 2 ? WL : 1];
+    // element e = (tid + 256 q) * LW -> row e / 64, k e % 64 (coalesced rows).
+    // NTH * LW is a multiple of BK, so a thread's in-chunk k (kt) is the same for
+    // every q: per chunk one clamped k, and the row offsets (rows past n and
+    // past HF clamped: in-bounds loads that are never used) are hoisted.
+    static_assert((NTH * LW) % BK == 0, "one in-chunk k per thread");
+    const int kt = (tid * LW) % BK;
+    int xro[XL], wro[WL];
+    bool wok[WL];
+#pragma unroll
+    for (int q = 0; q < XL; ++q) xro[q] = min(blk0 + (tid + NTH * q) * LW / BK, n - 1) * fin;
+#pragma unroll
+    for (int q = 0; q < WL; ++q) {
+        const int e = (tid + NTH * q) * LW;
+        wro[q] = min(e / BK, HF - 1) * fin;
+        wok[q] = e / BK < HF && e < BN * BK;  // (e past the chunk: a clamped dummy)
+    }
     auto load_chunk = [&](int k0, vec (&xn)[XL], vec (&wn)[WL]) {
-        // element e = (tid + 256 q) * LW -> row e / 64, k e % 64 (coalesced rows);
-        // clamped, in-bounds addresses past n / fin (zeroed W meets them)
+        const int k = min(k0 + kt, fin - LW);  // clamped past fin (the tail chunk)
 #pragma unroll
-        for (int q = 0; q < XL; ++q) {
-            const int e = (tid + NTH * q) * LW;
-            const int r = min(blk0 + e / BK, n - 1);
-            const int k = min(k0 + e % BK, fin - LW);
-            xn[q] = *reinterpret_cast<const vec*>(X + (size_t)r * fin + k);
-        }
+        for (int q = 0; q < XL; ++q) xn[q] = *reinterpret_cast<const vec*>(X + xro[q] + k);
 #pragma unroll
-        for (int q = 0; q < WL; ++q) {
-            const int e = (tid + NTH * q) * LW;
-            const int nn = min(e / BK, HF - 1);  // (e past the chunk: a clamped dummy)
-            const int k = min(k0 + e % BK, fin - LW);
-            wn[q] = *reinterpret_cast<const vec*>(W + (size_t)nn * fin + k);
-        }
+        for (int q = 0; q < WL; ++q) wn[q] = *reinterpret_cast<const vec*>(W + wro[q] + k);
     };
     // x chunk to LDS as fp32; W chunk split into three bf16 planes
     auto stage = [&](int k0, const vec (&xn)[XL], const vec (&wn)[WL]) {
+        // k past fin (the tail chunk): the clamped loads hold real x of this row,
+        // which must not meet the zeroed W (an infinite x would give Inf * 0 = NaN).
+        // Whole chunks (block-uniform, a scalar branch) skip the selects.
+        const bool full = k0 + BK <= fin;
+        const bool kin = full || k0 + kt < fin;
+        if (full) {
 #pragma unroll
-        for (int q = 0; q < XL; ++q) {
-            // k past fin: the clamped load holds real x of this row, which must
-            // not meet the zeroed W (an infinite x would give Inf * 0 = NaN)
-            const int e = (tid + NTH * q) * LW;
-            *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) =
-                k0 + e % BK < fin ? xn[q] : vec{};
+            for (int q = 0; q < XL; ++q) {
+                const int e = (tid + NTH * q) * LW;
+                *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) = xn[q];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < XL; ++q) {
+                const int e = (tid + NTH * q) * LW;
+                *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) = kin ? xn[q] : vec{};
+            }
         }
 #pragma unroll
         for (int q = 0; q < WL; ++q) {
             const int e = (tid + NTH * q) * LW;
-            const bool ok = e / BK < HF && k0 + e % BK < fin && e < BN * BK;
+            const bool ok = wok[q] && kin;
             const int o = min(e / BK, BN - 1) * WSB + e % BK;
             if constexpr (LW == 1) {
                 bf16x2 p1, p2, p3;
