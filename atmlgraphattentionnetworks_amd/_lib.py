@@ -50,6 +50,10 @@ SIGNATURES = {
     "gat_project_chunked": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                      _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int, _c_int, _c_ll,
                                      _c_vp, _c_vp]),
+    "gat_project_workspace_size": (_c_int, [_c_int, _c_int, _c_int, _c_size_p]),
+    "gat_project_ex": (_c_int, [_c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                _c_int, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_int, _c_vp,
+                                _c_int, _c_ll, _c_vp, ctypes.c_size_t, _c_vp]),
     "gat_edge_aggregate_sliced": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_int,
                                            _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_float,
                                            _c_vp, _c_vp, _c_int, _c_vp]),
@@ -200,3 +204,11 @@ def bwd_sources_parts(num_nodes: int, heads: int, f: int) -> int:
     check(load().gat_bwd_sources_parts(num_nodes, heads, f, ctypes.byref(out)),
           "gat_bwd_sources_parts")
     return out.value
+
+
+def project_workspace_bytes(fin: int, heads: int, f: int) -> int:
+    """Bytes of the optional projection workspace (gat_project_workspace_size)."""
+    n = ctypes.c_size_t(0)
+    check(load().gat_project_workspace_size(fin, heads, f, ctypes.byref(n)),
+          "gat_project_workspace_size")
+    return int(n.value)

@@ -535,7 +535,41 @@ __device__ __forceinline__ void split3_x8(f32x4 a, f32x4 b, bf16x8& h1, bf16x8& 
         if (n <= 0) return;                                                       \
     }
 
-template <int NT, int LW, int RG, int PD, int MINB = 1>
+// W [HF, fin] split exactly into three bf16 planes [3][BN][KP] (KP =
+// round_up(fin, 64), zero past HF and fin): the pre-split operand of
+// k_project_x3<..., PS = true>.  One thread per 8 consecutive k of a column.
+__global__ __launch_bounds__(256) void k_split_w(const float* __restrict__ W, int HF, int fin,
+                                                int BN, int KP, __bf16* __restrict__ out) {
+    const int per_row = KP / 8;
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= BN * per_row) return;
+    const int c = u / per_row, k = (u % per_row) * 8;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (c < HF && k + j < fin) ? W[(size_t)c * fin + k + j] : 0.f;
+    bf16x8 h1, h2, h3;
+    split3_x8(f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}, h1, h2, h3);
+    const size_t o = (size_t)c * KP + k, plane = (size_t)BN * KP;
+    *reinterpret_cast<bf16x8*>(out + o) = h1;
+    *reinterpret_cast<bf16x8*>(out + plane + o) = h2;
+    *reinterpret_cast<bf16x8*>(out + 2 * plane + o) = h3;
+}
+
+// bytes of the pre-split W planes for (hf, fin): 0 where k_project_x3 does not
+// take them (fin <= 128, or column tiles other than 2 or 4)
+inline size_t wsplit_bytes(int hf, int fin) {
+    const int nt = (hf + 15) / 16;
+    if (fin <= 128 || (nt != 2 && nt != 4)) return 0;
+    return (size_t)3 * (size_t)(nt * 16) * (size_t)((fin + 63) / 64 * 64) * 2;
+}
+
+// PS (pre-split W): W points at the three bf16 planes gat_project_ex's
+// k_split_w wrote into the caller's workspace, [3][BN][KP] with KP =
+// round_up(fin, 64), zero past HF and fin: each chunk's W tile is copied into
+// LDS as it is (six 16-B loads per thread at BN = 64) instead of being loaded
+// as fp32 and split by every workgroup (the split was ~1/3 of the loop's VALU
+// work, which bounds this kernel at Reddit scale).
+template <int NT, int LW, int RG, int PD, int MINB = 1, bool PS = false>
 __global__ __launch_bounds__(256, MINB) void k_project_x3(
     const float* __restrict__ X, int n, int fin,
     const float* __restrict__ W, const float* __restrict__ bW,
@@ -568,34 +602,53 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
 #pragma unroll
         for (int t = 0; t < NT; ++t) acc[g][t] = cor[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // PS: the W tile in 16-B pieces of the pre-split planes
+    constexpr int WQ = PS ? 3 * BN * BK / (NTH * 8) : WL;
+    static_assert(!PS || (3 * BN * BK) % (NTH * 8) == 0, "pre-split W tile split");
+    using wvec = typename std::conditional<PS, u32x4, vec>::type;
     // PD chunks of loads in flight (PD = 2: a register double buffer,
     // statically indexed)
-    vec xa_[XL], wa_[WL], xb_[PD == 2 ? XL : 1], wb_[PD == 2 ? WL : 1];
+    vec xa_[XL], xb_[PD == 2 ? XL : 1];
+    wvec wa_[WQ], wb_[PD == 2 ? WQ : 1];
     // element e = (tid + 256 q) * LW -> row e / 64, k e % 64 (coalesced rows).
     // NTH * LW is a multiple of BK, so a thread's in-chunk k (kt) is the same for
     // every q: per chunk one clamped k, and the row offsets (rows past n and
     // past HF clamped: in-bounds loads that are never used) are hoisted.
     static_assert((NTH * LW) % BK == 0, "one in-chunk k per thread");
     const int kt = (tid * LW) % BK;
-    int xro[XL], wro[WL];
+    int xro[XL], wro[WQ];
     bool wok[WL];
 #pragma unroll
     for (int q = 0; q < XL; ++q) xro[q] = min(blk0 + (tid + NTH * q) * LW / BK, n - 1) * fin;
+    const int kp = (fin + BK - 1) / BK * BK;  // PS: padded K of the planes
 #pragma unroll
-    for (int q = 0; q < WL; ++q) {
-        const int e = (tid + NTH * q) * LW;
-        wro[q] = min(e / BK, HF - 1) * fin;
-        wok[q] = e / BK < HF && e < BN * BK;  // (e past the chunk: a clamped dummy)
+    for (int q = 0; q < WQ; ++q) {
+        if constexpr (PS) {
+            // 16-B piece u of the chunk's tile: plane u / (8 BN), column
+            // (u / 8) % BN, k 8 (u % 8) .. +8 (bf16 elements)
+            const int u = tid + NTH * q;
+            wro[q] = ((u / (8 * BN)) * BN + (u / 8) % BN) * kp + 8 * (u % 8);
+        } else {
+            const int e = (tid + NTH * q) * LW;
+            wro[q] = min(e / BK, HF - 1) * fin;
+            wok[q] = e / BK < HF && e < BN * BK;  // (e past the chunk: a clamped dummy)
+        }
     }
-    auto load_chunk = [&](int k0, vec (&xn)[XL], vec (&wn)[WL]) {
+    auto load_chunk = [&](int k0, vec (&xn)[XL], wvec (&wn)[WQ]) {
         const int k = min(k0 + kt, fin - LW);  // clamped past fin (the tail chunk)
 #pragma unroll
         for (int q = 0; q < XL; ++q) xn[q] = *reinterpret_cast<const vec*>(X + xro[q] + k);
 #pragma unroll
-        for (int q = 0; q < WL; ++q) wn[q] = *reinterpret_cast<const vec*>(W + wro[q] + k);
+        for (int q = 0; q < WQ; ++q) {
+            if constexpr (PS)
+                wn[q] = *reinterpret_cast<const u32x4*>(
+                    reinterpret_cast<const __bf16*>(W) + wro[q] + k0);
+            else
+                wn[q] = *reinterpret_cast<const vec*>(W + wro[q] + k);
+        }
     };
     // x chunk to LDS as fp32; W chunk split into three bf16 planes
-    auto stage = [&](int k0, const vec (&xn)[XL], const vec (&wn)[WL]) {
+    auto stage = [&](int k0, const vec (&xn)[XL], const wvec (&wn)[WQ]) {
         // k past fin (the tail chunk): the clamped loads hold real x of this row,
         // which must not meet the zeroed W (an infinite x would give Inf * 0 = NaN).
         // Whole chunks (block-uniform, a scalar branch) skip the selects.
@@ -614,6 +667,15 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
                 *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) = kin ? xn[q] : vec{};
             }
         }
+        if constexpr (PS) {
+#pragma unroll
+            for (int q = 0; q < WQ; ++q) {
+                const int u = tid + NTH * q;
+                *reinterpret_cast<u32x4*>(&wsb[u / (8 * BN)][((u / 8) % BN) * WSB + 8 * (u % 8)]) =
+                    wn[q];
+            }
+            return;
+        } else {
 #pragma unroll
         for (int q = 0; q < WL; ++q) {
             const int e = (tid + NTH * q) * LW;
@@ -640,6 +702,7 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
                 *reinterpret_cast<bf16x4*>(&wsb[1][o]) = bf16x4{p2a[0], p2a[1], p2b[0], p2b[1]};
                 *reinterpret_cast<bf16x4*>(&wsb[2][o]) = bf16x4{p3a[0], p3a[1], p3b[0], p3b[1]};
             }
+        }
         }
     };
     auto compute = [&](int k0) {
@@ -1355,6 +1418,13 @@ __global__ __launch_bounds__(256) void k_project_wk(
     }
 }
 
+// k_project_x3 on pre-split W (instantiated for 2 and 4 column tiles only)
+template <int NT, int LW, class... A>
+static void launch_x3_presplit(dim3 grid, dim3 block, hipStream_t st, A... a) {
+    if constexpr (NT == 2 || NT == 4)
+        hipLaunchKernelGGL((k_project_x3<NT, LW, 1, 1, 1, true>), grid, block, 0, st, a...);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1366,7 +1436,8 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
                         const float* a_src, const float* c_src, const float* a_dst,
                         const float* c_dst, int heads, int f, int slices, float* wh, int ld_wh,
                         float* s_src, int ld_s, float* s_dst, void* stream, int n_table = 0,
-                        int crows = 0, long long cjump = 0) {
+                        int crows = 0, long long cjump = 0, void* ws = nullptr,
+                        size_t ws_bytes = 0) {
     if (n < 0 || fin < 0 || heads <= 0 || f <= 0 || slices <= 0) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
@@ -1547,13 +1618,32 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #else
 #define GAT_PIPE2_FP32(NT, LWV) (void)gp
 #endif
+        // W pre-split once per call into the caller's workspace (gat_project_ex):
+        // the default x3 form then stages bf16 W tiles without splitting them
+        // (GAT_PROJ_PRESPLIT=0, A/B knob: split per workgroup as before)
+        const size_t need = wsplit_bytes(hf, fin);
+        bool presplit = x3 && ws != nullptr && need > 0 && ws_bytes >= need && x3v == 1 &&
+                        (reinterpret_cast<uintptr_t>(ws) & 15) == 0;
+        if (const char* v = knob("GAT_PROJ_PRESPLIT")) presplit = presplit && std::atoi(v) != 0;
+        if (presplit) {
+            const int bn = nt * 16, kpad = (fin + 63) / 64 * 64;
+            const int units = bn * (kpad / 8);
+            hipLaunchKernelGGL(k_split_w, dim3((units + 255) / 256), dim3(256), 0, st, w, hf, fin, bn,
+                               kpad, reinterpret_cast<__bf16*>(ws));
+        }
 #define GAT_X3V(NT, LWV, RGV, PDV, MB, BMV)                                                   \
     hipLaunchKernelGGL((k_project_x3<NT, LWV, RGV, PDV, MB>), dim3((nr + BMV - 1) / BMV, ny), bp, \
                        0, st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,   \
                        ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows,     \
                        cjump)
+#define GAT_X3PS(NT, LWV)                                                                      \
+    launch_x3_presplit<NT, LWV>(dim3((nr + 63) / 64, ny), bp, st, x, n, fin,                    \
+                                reinterpret_cast<const float*>(ws), b, a_src, c_src, a_dst, c_dst, \
+                                heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst, slice_w,           \
+                                slice_stride, store_wt, crows, cjump)
 #define GAT_PIPE2(NT, LWV)                                                                     \
-    if (x3 && x3v == 1) GAT_X3V(NT, LWV, 1, 1, 1, 64);                                         \
+    if (x3 && presplit && (NT == 2 || NT == 4)) GAT_X3PS(NT, LWV);                             \
+    else if (x3 && x3v == 1) GAT_X3V(NT, LWV, 1, 1, 1, 64);                                    \
     else if (x3 && x3v == 2) GAT_X3V(NT, LWV, 1, 1, 3, 64);                                    \
     else if (x3 && x3v == 3) GAT_X3V(NT, LWV, 2, 1, 2, 128);                                   \
     else if (x3 && x3v == 4) GAT_X3V(NT, LWV, 1, 2, 2, 64);                                    \
@@ -1580,6 +1670,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #undef GAT_PIPE2
 #undef GAT_PIPE2_FP32
 #undef GAT_X3V
+#undef GAT_X3PS
         return status_of(hipGetLastError());
     }
     if (sliced || ny > 1) return GAT_EUNSUPPORTED;  // the kernels below: row-major Wh, no chunks
@@ -1636,6 +1727,32 @@ int gat_project_chunked(const float* x, int n, int fin, const float* w, const fl
     return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
                         heads * f / slices, nullptr, heads, s_dst, stream, plane_rows, chunk_rows,
                         chunk_stride);
+}
+
+int gat_project_workspace_size(int fin, int heads, int f, size_t* bytes) {
+    if (bytes == nullptr || fin < 0 || heads <= 0 || f <= 0) return GAT_EINVAL;
+    *bytes = wsplit_bytes(heads * f, fin);
+    return GAT_OK;
+}
+
+int gat_project_ex(const float* x, int n, int fin, const float* w, const float* b,
+                   const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,
+                   int heads, int f, int slices, float* wh, int ld_wh_or_n_table, float* s_src,
+                   int ld_s, float* s_dst, int chunk_rows, long long chunk_stride,
+                   void* workspace, size_t workspace_bytes, void* stream) {
+    if (slices <= 0 || heads <= 0 || f <= 0 || (heads * f) % slices != 0 || chunk_rows < 0)
+        return GAT_EINVAL;
+    if (chunk_rows > 0 && (slices <= 1 || ld_wh_or_n_table < chunk_rows ||
+                           chunk_stride < (long long)slices * ld_wh_or_n_table * (heads * f / slices)))
+        return GAT_EINVAL;
+    if (slices == 1)
+        return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, 1, wh,
+                            ld_wh_or_n_table, s_src, ld_s, s_dst, stream, 0, 0, 0, workspace,
+                            workspace_bytes);
+    if (s_src == nullptr) ld_s = heads;
+    return project_impl(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
+                        heads * f / slices, s_src, ld_s, s_dst, stream, ld_wh_or_n_table,
+                        chunk_rows, chunk_stride, workspace, workspace_bytes);
 }
 
 }  // extern "C"

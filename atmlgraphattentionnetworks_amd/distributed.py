@@ -162,8 +162,16 @@ class HipOps:
     """The HIP kernels (default)."""
 
     @staticmethod
-    def project_rows(x, pp, heads, f, layout: TableLayout, table, offset, s_dst, s_scratch):
-        """Project rows x into the table block at float offset ``offset``."""
+    def workspace(x_device, fin: int, heads: int, f: int):
+        """The projection's optional workspace (gat_project_ex), or None."""
+        from .layer import project_workspace
+        return project_workspace(x_device, fin, heads, f)
+
+    @staticmethod
+    def project_rows(x, pp, heads, f, layout: TableLayout, table, offset, s_dst, s_scratch,
+                     ws=None):
+        """Project rows x into the table block at float offset ``offset``
+        (gat_project_ex; ``ws`` its optional workspace)."""
         lib = _lib.load()
         n, fin = x.shape
         if n == 0:
@@ -172,33 +180,35 @@ class HipOps:
         wh = table.data_ptr() + 4 * offset
         args = (x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(),
                 pp.c_src.data_ptr(), pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f)
+        wsa = (0, 0) if ws is None else (ws.data_ptr(), ws.numel())
         if layout.kind == "planes":
-            rc = lib.gat_project_sliced(*args, layout.slices, wh, layout.block_rows, 0, heads,
-                                        s_dst.data_ptr(), stream)
+            rc = lib.gat_project_ex(*args, layout.slices, wh, layout.block_rows, 0, heads,
+                                    s_dst.data_ptr(), 0, 0, *wsa, stream)
         elif layout.kind == "wh":
-            rc = lib.gat_project(*args, wh, layout.width, s_scratch.data_ptr(), heads,
-                                 s_dst.data_ptr(), stream)
+            rc = lib.gat_project_ex(*args, 1, wh, layout.width, s_scratch.data_ptr(), heads,
+                                    s_dst.data_ptr(), 0, 0, *wsa, stream)
         else:
-            rc = lib.gat_project(*args, wh, layout.width, wh + 4 * layout.s_off, layout.width,
-                                 s_dst.data_ptr(), stream)
-        _lib.check(rc, "gat_project (shard block)")
+            rc = lib.gat_project_ex(*args, 1, wh, layout.width, wh + 4 * layout.s_off,
+                                    layout.width, s_dst.data_ptr(), 0, 0, *wsa, stream)
+        _lib.check(rc, "gat_project_ex (shard block)")
 
     @staticmethod
-    def project_chunked(x, pp, heads, f, layout: TableLayout, table, rank: int, s_dst):
-        """All of a rank's rows in ONE launch (gat_project_chunked): row chunk c
-        goes to the rank's block of table chunk c (planes layout only)."""
+    def project_chunked(x, pp, heads, f, layout: TableLayout, table, rank: int, s_dst, ws=None):
+        """All of a rank's rows in ONE launch (gat_project_ex with row chunks):
+        row chunk c goes to the rank's block of table chunk c (planes only)."""
         lib = _lib.load()
         n, fin = x.shape
         if n == 0:
             return
         stream = torch._C._cuda_getCurrentRawStream(x.device.index)
-        rc = lib.gat_project_chunked(
+        wsa = (0, 0) if ws is None else (ws.data_ptr(), ws.numel())
+        rc = lib.gat_project_ex(
             x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(),
             pp.c_src.data_ptr(), pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
             layout.slices, table.data_ptr() + 4 * layout.block_offset(0, rank),
-            layout.block_rows, layout.block_rows, layout.world * layout.block_floats,
-            s_dst.data_ptr(), stream)
-        _lib.check(rc, "gat_project_chunked (shard)")
+            layout.block_rows, 0, heads, s_dst.data_ptr(), layout.block_rows,
+            layout.world * layout.block_floats, *wsa, stream)
+        _lib.check(rc, "gat_project_ex (shard, row chunks)")
 
     @staticmethod
     def edge_pass(local: LocalCSR, c: int, layout: TableLayout, table, s_dst, pp, bias, heads,
@@ -368,6 +378,9 @@ class ShardedGAT:
                                      device=dev)
         else:
             self.st_acc = self.st_ml = None
+        # the projection's optional workspace (HIP ops only; CPU stand-ins take none)
+        self.pws = (self.ops.workspace(dev, layer.input_channels, heads, f)
+                    if hasattr(self.ops, "workspace") else None)
         if exchanger is None:
             exchanger = CollectiveExchange(group) if (
                 exchange == "allgather" and (world > 1 or self.force_exchange)) else NoExchange()
@@ -419,14 +432,18 @@ class ShardedGAT:
         lay = self.layout
         if self.exchange == "replicate":
             self.ops.project_rows(xl, self.pp, self.heads, self.f, lay, self.table, 0,
-                                  self.s_dst, self.s_scratch)
+                                  self.s_dst, self.s_scratch, **self._ws_kw())
             return
         lo = c * lay.block_rows
         hi = min(lo + lay.block_rows, self.n_local)
         if hi <= lo:
             return
         self.ops.project_rows(xl[lo:hi], self.pp, self.heads, self.f, lay, self.table,
-                              lay.block_offset(c, self.rank), self.s_dst[lo:hi], self.s_scratch)
+                              lay.block_offset(c, self.rank), self.s_dst[lo:hi], self.s_scratch,
+                              **self._ws_kw())
+
+    def _ws_kw(self):
+        return {} if self.pws is None else {"ws": self.pws}
 
     def project_all(self, xl) -> None:
         """Every chunk's projection: one launch over all of the rank's rows
@@ -437,7 +454,7 @@ class ShardedGAT:
         if (self.exchange == "allgather" and lay.kind == "planes" and self.chunks > 1
                 and hasattr(self.ops, "project_chunked") and lay.block_rows % 64 == 0):
             self.ops.project_chunked(xl, self.pp, self.heads, self.f, lay, self.table,
-                                     self.rank, self.s_dst)
+                                     self.rank, self.s_dst, **self._ws_kw())
             return
         for c in range(self.chunks):
             self.project_chunk(xl, c)

@@ -158,31 +158,40 @@ def alloc_table(n: int, heads: int, f: int, device, packed: bool = False,
     return NodeTable(wh, hfp, s_src, heads)
 
 
+def project_workspace(device, fin: int, heads: int, f: int) -> Optional[torch.Tensor]:
+    """The optional workspace of ``gat_project_ex`` (Fin > 128: W split into
+    bf16 planes once per launch instead of in every workgroup), or None."""
+    nb = _lib.project_workspace_bytes(fin, heads, f)
+    return torch.empty(nb, dtype=torch.uint8, device=device) if nb > 0 else None
+
+
 def project(x: torch.Tensor, pp: PackedParams, heads: int, f: int,
             table: Optional[NodeTable] = None, s_dst: Optional[torch.Tensor] = None):
-    """``gat_project``: node table (Wh, s_src) and s_dst [N, H]."""
+    """``gat_project_ex``: node table (Wh, s_src) and s_dst [N, H]."""
     lib = _lib.load()
     n, fin = x.shape
     if table is None:
         table = alloc_table(n, heads, f, x.device)
     if s_dst is None:
         s_dst = torch.empty(n, heads, dtype=torch.float32, device=x.device)
+    ws = project_workspace(x.device, fin, heads, f)
+    wsa = (0, 0) if ws is None else (ws.data_ptr(), ws.numel())
+    args = (x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(),
+            pp.c_src.data_ptr(), pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f)
     if table.slices > 1:
         # planes of wh.stride(0) / ld_wh rows; wh may be a rank's slot (rows view)
-        _lib.check(lib.gat_project_sliced(
-            x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(), pp.a_src.data_ptr(),
-            pp.c_src.data_ptr(), pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
-            table.slices, table.wh.data_ptr(), table.wh.stride(0) // table.ld_wh, 0, heads,
-            s_dst.data_ptr(), _stream(x.device)), "gat_project_sliced")
+        _lib.check(lib.gat_project_ex(*args, table.slices, table.wh.data_ptr(),
+                                      table.wh.stride(0) // table.ld_wh, 0, heads,
+                                      s_dst.data_ptr(), 0, 0, *wsa, _stream(x.device)),
+                   "gat_project_ex (planes)")
         return table, s_dst
     s_src = table.s_src
     if s_src is None:  # Wh-only table: the scores still have to go somewhere
         s_src = torch.empty(n, heads, dtype=torch.float32, device=x.device)
-    _lib.check(lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
-                               pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                               pp.c_dst.data_ptr(), heads, f, table.wh.data_ptr(), table.ld_wh,
-                               s_src.data_ptr(), heads if table.s_src is None else table.ld_s,
-                               s_dst.data_ptr(), _stream(x.device)), "gat_project")
+    _lib.check(lib.gat_project_ex(*args, 1, table.wh.data_ptr(), table.ld_wh, s_src.data_ptr(),
+                                  heads if table.s_src is None else table.ld_s,
+                                  s_dst.data_ptr(), 0, 0, *wsa, _stream(x.device)),
+               "gat_project_ex")
     return table, s_dst
 
 
@@ -312,7 +321,7 @@ class ForwardPlan:
 
     __slots__ = ("n", "fin", "heads", "f", "hf", "hfp", "concat", "slope", "slices", "split",
                  "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched", "_csr", "bound",
-                 "bufs", "cur")
+                 "bufs", "cur", "pws")
 
     def __init__(self, x: torch.Tensor, csr: CSRGraph, heads: int, f: int, concat: bool,
                  negative_slope: float, pingpong: bool = False):
@@ -333,6 +342,9 @@ class ForwardPlan:
             self.bufs.append((p_wh, p_ss, p_ss + 4 * n * heads))
         self.cur = 0
         self.p_wh, self.p_ss, self.p_sd = self.bufs[0]
+        # the projection's optional workspace (Fin > 128: W split into bf16
+        # planes once per call; gat_project_ex), or None
+        self.pws = project_workspace(x.device, fin, heads, f)
         self.dev = x.device.index
         self.hint = csr.num_edges // max(n, 1)
         self.slices = wh_slices(heads, f, concat, negative_slope, self.hint)
@@ -398,9 +410,21 @@ class ForwardPlan:
         return (pp, bias.data_ptr(), lib, lib.gat_layer_forward, fargs, self.slices > 1)
 
     def project(self, lib, x: torch.Tensor, pp: PackedParams) -> None:
-        """gat_project(_sliced) into the workspace (GAT.py:42-52)."""
+        """gat_project(_sliced / _ex) into the workspace (GAT.py:42-52)."""
         n, fin, heads, f = self.n, self.fin, self.heads, self.f
         stream = torch._C._cuda_getCurrentRawStream(self.dev)  # the current stream, per call
+        if self.pws is not None:
+            ld = n if self.slices > 1 else self.hfp
+            rc = lib.gat_project_ex(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                                    pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+                                    pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
+                                    self.slices, self.p_wh, ld, self.p_ss, heads, self.p_sd, 0, 0,
+                                    self.pws.data_ptr(), self.pws.numel(), stream)
+            if rc == 0:
+                return
+            if rc != _lib.GAT_EUNSUPPORTED or self.slices == 1:
+                _lib.check(rc, "gat_project_ex")
+            self.slices = 1  # nothing was launched: the row-major table instead
         if self.slices > 1:
             rc = lib.gat_project_sliced(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                         pp.a_src.data_ptr(), pp.c_src.data_ptr(),

@@ -96,12 +96,16 @@ class GATFunction(torch.autograd.Function):
         s_dst = ws[o + n * heads:o + 2 * n * heads].view(n, heads)
         lse = ws[o + 2 * n * heads:o + 3 * n * heads].view(n, heads)
         y = ws[o + 3 * n * heads:o + 3 * n * heads + n * hf].view(n, hf)
-        rc = lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
-                             pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                             pp.c_dst.data_ptr(), heads, f, wh.data_ptr(), hfp,
-                             s_src.data_ptr(), heads, s_dst.data_ptr(), stream)
+        from .layer import project_workspace
+        pws = project_workspace(dev, fin, heads, f)
+        rc = lib.gat_project_ex(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                                pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
+                                pp.c_dst.data_ptr(), heads, f, 1, wh.data_ptr(), hfp,
+                                s_src.data_ptr(), heads, s_dst.data_ptr(), 0, 0,
+                                0 if pws is None else pws.data_ptr(),
+                                0 if pws is None else pws.numel(), stream)
         if rc:
-            _lib.check(rc, "gat_project")
+            _lib.check(rc, "gat_project_ex")
         out = torch.empty(n, hf if concat else f, dtype=torch.float32, device=dev)
         order = csr.order
         if kink:

@@ -177,6 +177,26 @@ int gat_project_chunked(const float* x, int n, int fin, const float* w, const fl
                         const float* c_dst, int heads, int f, int slices, float* wh,
                         int plane_rows, int chunk_rows, long long chunk_stride, float* s_dst,
                         void* stream);
+/*
+ * gat_project_ex (ABI 8): every projection layout in one entry point, with an
+ * optional caller-owned workspace.  slices == 1: Wh row-major with ld_wh =
+ * ld_wh_or_n_table (as gat_project; s_src [n, ld_s] may not be NULL).  slices
+ * > 1: planes of n_table = ld_wh_or_n_table rows (as gat_project_sliced; s_src
+ * may be NULL), and with chunk_rows > 0 the row chunks of gat_project_chunked
+ * (chunk_stride floats apart).  workspace (16-B aligned, workspace_bytes >=
+ * gat_project_workspace_size's bytes) lets the Fin > 128 kernel split W into
+ * bf16 planes once per call instead of once per workgroup; NULL (or a smaller
+ * buffer) runs the same kernels as the other entry points.  Results are
+ * identical either way (the split is exact).
+ * gat_project_workspace_size: the bytes for (fin, heads, f): 0 where the
+ * projection takes no workspace (fin <= 128, or heads*f not in (16, 64]).
+ */
+int gat_project_workspace_size(int fin, int heads, int f, size_t* bytes);
+int gat_project_ex(const float* x, int n, int fin, const float* w, const float* b,
+                   const float* a_src, const float* c_src, const float* a_dst, const float* c_dst,
+                   int heads, int f, int slices, float* wh, int ld_wh_or_n_table, float* s_src,
+                   int ld_s, float* s_dst, int chunk_rows, long long chunk_stride,
+                   void* workspace, size_t workspace_bytes, void* stream);
 int gat_edge_aggregate_sliced(const int* rowptr, const int* col, const int* row_order,
                               int row_begin, int row_end, const float* wh, int n_table,
                               int slices, const float* a_src, const float* c_src,

@@ -49,6 +49,10 @@ VARIANTS = {
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
     "proj_wk_lds_epilogue": {"GAT_PROJ_WK_DIRECT": "0"},
     "plain_stores": {"GAT_STORE_WT": "0"},
+    # Fin > 128: W split per workgroup instead of pre-split once per launch
+    # (gat_project_ex's workspace); the pre-split form for 4-float / 1-float rows
+    "proj_nopresplit": {"GAT_PROJ_PRESPLIT": "0"},
+    "proj_x3_b64p1": {"GAT_PROJ_X3V": "b64p1"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
 }
@@ -60,7 +64,8 @@ def variant(request, monkeypatch):
               "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
-              "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA"):
+              "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
+              "GAT_PROJ_PRESPLIT"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -121,6 +126,9 @@ CASES = [
     (64, 0, 5, 4, 8, True, "uniform"),  # self-loops only
     (1, 0, 3, 2, 2, True, "uniform"),  # a single node
     (700, 9000, 602, 8, 8, True, "uniform"),  # Reddit's Fin
+    # pre-split W (Fin > 128, HF 32 / 64): K tails, mean mode
+    (500, 5000, 202, 4, 8, True, "uniform"),
+    (321, 4000, 138, 8, 8, False, "uniform"),
     # the K-chunked projections (Fin > 128; Fin > 64 with GAT_PROJ_WRES=0): K tails and
     # partial column tiles
     (400, 5000, 65, 4, 8, True, "uniform"),  # one-column tail chunk, NT = 2
@@ -359,6 +367,67 @@ def test_sliced_default_with_unaligned_x_view():
                                 pp.c_dst.data_ptr(), H, F, 2, wh.data_ptr(), n, None, H,
                                 sd.data_ptr(), torch.cuda.current_stream().cuda_stream)
     assert rc == _lib.GAT_EUNSUPPORTED
+
+
+@pytest.mark.parametrize("fin,heads,x3v", [(602, 8, None), (138, 4, None), (602, 8, "b64p1"),
+                                           (200, 8, "b64p1"), (201, 4, "b64p1"),
+                                           (602, 4, "b64p1w3")])
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_projection_presplit_bitwise(fin, heads, x3v, chunks, monkeypatch):
+    """gat_project_ex with its workspace (W split once per launch, k_split_w)
+    equals the per-workgroup split bitwise (the same exact 3-term split), for
+    row-major and planes tables, one launch over row chunks included; without a
+    workspace, or one too small, it falls back to the per-workgroup split."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, _lib, tuning
+    from atmlgraphattentionnetworks_amd.layer import project_workspace
+    d = dev()
+    torch.manual_seed(1)
+    F, n = 8, 1000
+    hf = heads * F
+    layer = GraphAttentionLayer(fin, F, num_heads=heads, concat=True).to(d).eval()
+    pp = layer.packed()
+    x = torch.randn(n, fin, device=d)
+    ws = project_workspace(d, fin, heads, F)
+    assert ws is not None and ws.numel() == 3 * hf * ((fin + 63) // 64 * 64) * 2
+    lib = _lib.load()
+    for slices in (1, 2):
+        if chunks > 1 and slices == 1:
+            continue  # row chunks are a planes-table form
+        crows = ((n + chunks - 1) // chunks + 63) // 64 * 64 if chunks > 1 else 0
+        outs = []
+        for presplit, wsa in (("1", (ws.data_ptr(), ws.numel())), ("0", (ws.data_ptr(), ws.numel())),
+                              ("1", (0, 0)), ("1", (ws.data_ptr(), ws.numel() - 16))):
+            monkeypatch.setenv("GAT_PROJ_PRESPLIT", presplit)
+            if x3v:
+                monkeypatch.setenv("GAT_PROJ_X3V", x3v)
+            tuning.reload()
+            # row chunk c of ``crows`` rows goes to block c of (n rounded) rows
+            blk = crows if crows else n
+            nblk = (n + blk - 1) // blk
+            wh = torch.full((nblk * blk * hf + 64,), float("nan"), device=d)
+            ss = torch.full((n * heads,), float("nan"), device=d)
+            sd = torch.full((n * heads,), float("nan"), device=d)
+            ld = blk if slices > 1 else hf
+            jump = blk * hf if crows else 0
+            rc = lib.gat_project_ex(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
+                                    pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
+                                    pp.c_dst.data_ptr(), heads, F, slices, wh.data_ptr(), ld,
+                                    0 if slices > 1 else ss.data_ptr(), heads, sd.data_ptr(),
+                                    crows, jump, *wsa, torch.cuda.current_stream().cuda_stream)
+            _lib.check(rc, "gat_project_ex")
+            torch.cuda.synchronize()
+            outs.append((wh.cpu(), sd.cpu(), ss.cpu()))
+        for o in outs[1:]:
+            for a, b in zip(outs[0], o):
+                assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
+        if slices == 1 and crows == 0:
+            # and it is the reference's per-head fp32 Linears (GAT.py:43-45)
+            with torch.no_grad():
+                ref = torch.cat([torch.nn.functional.linear(x, layer.ws[h].weight,
+                                                            layer.ws[h].bias)
+                                 for h in range(heads)], 1).cpu()
+            torch.testing.assert_close(outs[0][0][:n * hf].view(n, hf), ref,
+                                       atol=1e-5, rtol=1e-5)
 
 
 @pytest.mark.parametrize("fin,kernel", [(50, None), (50, "tiled"), (128, None), (100, None),

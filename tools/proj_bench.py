@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Projection kernel timing over shapes x knob variants (interleaved rounds,
-each measurement a captured HIP graph of --iters launches), outputs checked
+"""Projection kernel timing over shapes x knob variants (gat_project_ex with its
+workspace; interleaved rounds, each measurement a captured HIP graph of --iters launches), outputs checked
 bitwise against the first variant (or within 1e-5 of it when a variant
 changes the arithmetic, e.g. another kernel).
 
@@ -77,21 +77,22 @@ def main():
             ss = torch.empty(n * H, device=dev)
             outs.append((wh, sd, ss))
 
+        from atmlgraphattentionnetworks_amd.layer import project_workspace
+        pws = project_workspace(dev, w.in_channels, H, F)
+        wsa = (0, 0) if pws is None else (pws.data_ptr(), pws.numel())
+
         def launch(i):
             wh, sd, ss = outs[i]
             st = torch.cuda.current_stream().cuda_stream  # the capture stream inside a graph
+            args = (x.data_ptr(), n, w.in_channels, pp.w.data_ptr(), pp.b.data_ptr(),
+                    pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
+                    pp.c_dst.data_ptr(), H, F)
             if slices > 1:
-                rc = lib.gat_project_sliced(x.data_ptr(), n, w.in_channels, pp.w.data_ptr(),
-                                            pp.b.data_ptr(), pp.a_src.data_ptr(),
-                                            pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                                            pp.c_dst.data_ptr(), H, F, slices, wh.data_ptr(), n,
-                                            0, H, sd.data_ptr(), st)
+                rc = lib.gat_project_ex(*args, slices, wh.data_ptr(), n, 0, H, sd.data_ptr(),
+                                        0, 0, *wsa, st)
             else:
-                rc = lib.gat_project(x.data_ptr(), n, w.in_channels, pp.w.data_ptr(),
-                                     pp.b.data_ptr(), pp.a_src.data_ptr(), pp.c_src.data_ptr(),
-                                     pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), H, F,
-                                     wh.data_ptr(), (hf + 3) // 4 * 4, ss.data_ptr(), H,
-                                     sd.data_ptr(), st)
+                rc = lib.gat_project_ex(*args, 1, wh.data_ptr(), (hf + 3) // 4 * 4,
+                                        ss.data_ptr(), H, sd.data_ptr(), 0, 0, *wsa, st)
             if rc:
                 raise RuntimeError(f"projection rc={rc}")
 
