@@ -18,7 +18,7 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 8
+GAT_ABI_VERSION = 9
 GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
 GAT_SEG_LOAD = 1
 GAT_SEG_STORE = 2
@@ -63,6 +63,8 @@ SIGNATURES = {
                                         _c_int, _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_edge_merge": (_c_int, [_c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_int, _c_int,
                                 _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+    "gat_edge_merge_ex": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_int,
+                                   _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gat_csr_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csr_build": (_c_int, [_c_vp, _c_ll, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, ctypes.c_size_t,
                                _c_vp, _c_vp]),

@@ -735,13 +735,16 @@ __global__ __launch_bounds__(256) void k_edge_lds(
 // Merge of split hub rows (degree skew).  A target row with more in-edges
 // than one lane group should walk serially is cut into segments that run as
 // separate virtual rows of k_edge_grp (EdgeRows by_pos + store), in parallel;
-// hub k's segment states are virtual rows [vptr[k], vptr[k+1]).  Per head:
+// hub k's segment states are virtual rows [vptr[k], vptr[k+1]) (through
+// vslot when given: segment j's state at vslot[j], the schedule position the
+// segment ran at when the segments are not scheduled hub by hub).  Per head:
 //   M = max_s m_s,  L = sum_s l_s 2^(m_s - M),  y = sum_s acc_s 2^(m_s - M) / (L + 1e-16)
 // which is the segmented softmax of PyG utils.softmax (GAT.py:60) regrouped.
 // One wave per hub row; the segment loop is short (<= a few hundred).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_edge_merge(
-    const int* __restrict__ hub_rows, const int* __restrict__ vptr, int n_hub,
+    const int* __restrict__ hub_rows, const int* __restrict__ vptr,
+    const int* __restrict__ vslot, int n_hub,
     const float* __restrict__ st_acc, int ld_st, const float* __restrict__ st_ml, int H, int F,
     int HF, int concat, const float* __restrict__ bias, float* __restrict__ out, int ld_out,
     float* __restrict__ lse, float* __restrict__ y_heads) {
@@ -750,13 +753,14 @@ __global__ __launch_bounds__(64) void k_edge_merge(
     if (k >= n_hub) return;
     const int lane = threadIdx.x;
     const int r = hub_rows[k], s0 = vptr[k], s1 = vptr[k + 1];
+#define SLOT(sg) (vslot != nullptr ? vslot[sg] : (sg))
     for (int h = lane; h < H; h += kWave) {
         float M = -INFINITY;
-        for (int sg = s0; sg < s1; ++sg) M = fmaxf(M, st_ml[(size_t)sg * 2 * H + h]);
+        for (int sg = s0; sg < s1; ++sg) M = fmaxf(M, st_ml[(size_t)SLOT(sg) * 2 * H + h]);
         float L = 0.f;
         for (int sg = s0; sg < s1; ++sg) {
-            const float ms = st_ml[(size_t)sg * 2 * H + h];
-            if (ms != -INFINITY) L += st_ml[(size_t)sg * 2 * H + H + h] * __builtin_amdgcn_exp2f(ms - M);
+            const float ms = st_ml[(size_t)SLOT(sg) * 2 * H + h];
+            if (ms != -INFINITY) L += st_ml[(size_t)SLOT(sg) * 2 * H + H + h] * __builtin_amdgcn_exp2f(ms - M);
         }
         Ms[h] = M;
         Ls[h] = L;
@@ -768,8 +772,8 @@ __global__ __launch_bounds__(64) void k_edge_merge(
         const float M = Ms[h];
         float a = 0.f;
         for (int sg = s0; sg < s1; ++sg) {
-            const float ms = st_ml[(size_t)sg * 2 * H + h];
-            if (ms != -INFINITY) a += st_acc[(size_t)sg * ld_st + cc] * __builtin_amdgcn_exp2f(ms - M);
+            const float ms = st_ml[(size_t)SLOT(sg) * 2 * H + h];
+            if (ms != -INFINITY) a += st_acc[(size_t)SLOT(sg) * ld_st + cc] * __builtin_amdgcn_exp2f(ms - M);
         }
         const float y = a / (Ls[h] + 1e-16f);
         if (y_heads != nullptr) y_heads[(size_t)r * HF + cc] = y;
@@ -784,6 +788,7 @@ __global__ __launch_bounds__(64) void k_edge_merge(
             out[(size_t)r * ld_out + f] = sum / (float)H + bias[f];
         }
     }
+#undef SLOT
 }
 
 }  // namespace
@@ -1196,6 +1201,13 @@ int gat_edge_aggregate_seg(const int* seg_begin, const int* seg_end, int seg_by_
 int gat_edge_merge(const int* hub_rows, const int* seg_ptr, int n_hub, const float* st_acc,
                    const float* st_ml, int heads, int f, int concat, const float* bias,
                    float* out, float* lse, float* y_heads, void* stream) {
+    return gat_edge_merge_ex(hub_rows, seg_ptr, nullptr, n_hub, st_acc, st_ml, heads, f, concat,
+                             bias, out, lse, y_heads, stream);
+}
+
+int gat_edge_merge_ex(const int* hub_rows, const int* seg_ptr, const int* seg_slot, int n_hub,
+                      const float* st_acc, const float* st_ml, int heads, int f, int concat,
+                      const float* bias, float* out, float* lse, float* y_heads, void* stream) {
     if (heads <= 0 || f <= 0 || n_hub < 0) return GAT_EINVAL;
     const int hf = heads * f;
     if (hf > GAT_MAX_HF || heads > GAT_MAX_HEADS) return GAT_EUNSUPPORTED;
@@ -1204,7 +1216,7 @@ int gat_edge_merge(const int* hub_rows, const int* seg_ptr, int n_hub, const flo
         bias == nullptr || out == nullptr)
         return GAT_EINVAL;
     hipLaunchKernelGGL(k_edge_merge, dim3(n_hub), dim3(kWave), 0, (hipStream_t)stream, hub_rows,
-                       seg_ptr, n_hub, st_acc, round_up4(hf), st_ml, heads, f, hf, concat, bias,
+                       seg_ptr, seg_slot, n_hub, st_acc, round_up4(hf), st_ml, heads, f, hf, concat, bias,
                        out, concat ? hf : f, lse, y_heads);
     return status_of(hipGetLastError());
 }

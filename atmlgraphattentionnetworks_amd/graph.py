@@ -36,6 +36,9 @@ class HubPlan(NamedTuple):
     sched_row: torch.Tensor  # int32 [n_vrows + N - n_hub]: target row per position
     sched_b: torch.Tensor  # int32: CSR range of each position
     sched_e: torch.Tensor
+    # int32 [n_vrows]: schedule position (= state row) of segment j in hub order,
+    # or None when the segments run hub by hub (position j)
+    seg_slot: Optional[torch.Tensor] = None
 
 
 class CSRGraph(NamedTuple):
@@ -92,7 +95,8 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int,
         # PyG's index_select raises on the same input (GAT.py:53 -> __lift__)
         raise ValueError(f"edge_index contains node ids outside [0, {num_nodes})")
     return CSRGraph(rowptr, col, num_nodes, E + num_nodes, order,
-                    hub_plan(rowptr, order, E + num_nodes), locality_hint(rowptr, col, num_nodes))
+                    hub_plan(rowptr, order, E + num_nodes, col=col),
+                    locality_hint(rowptr, col, num_nodes))
 
 
 def locality_hint(rowptr: torch.Tensor, col: torch.Tensor, num_nodes: int,
@@ -128,7 +132,8 @@ def hub_segment_len(num_edges: int) -> int:
 
 
 def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
-             seg_len: Optional[int] = None) -> Optional[HubPlan]:
+             seg_len: Optional[int] = None, col: Optional[torch.Tensor] = None
+             ) -> Optional[HubPlan]:
     """The split schedule for rows with more than 2 * seg_len in-edges, or
     None when there are none (every uniform BASELINE graph).  ``order`` is
     the degree-descending row order, so the hubs are its first rows.
@@ -153,11 +158,24 @@ def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
     vb = rp[hub_rows][vhub] + k * seg
     ve = torch.minimum(vb + seg, rp[hub_rows + 1][vhub])
     rest = o[n_hub:]
+    if tuning.get("GAT_ROW_ORDER") == "asc":  # A/B knob: whole rows by ascending degree
+        rest = rest.flip(0)
     i32 = torch.int32
+    vrow = hub_rows[vhub]
+    slot = None
+    if tuning.get("GAT_HUB_ORDER") == "src" and col is not None:
+        # segments by the first source id they gather (stable): the segments
+        # running together then sweep the same part of the node table, as
+        # equal-length whole rows do (ascending sources within every row)
+        perm = torch.sort(col[vb].to(torch.int64), stable=True).indices
+        vrow, vb, ve = vrow[perm], vb[perm], ve[perm]
+        slot = torch.empty(n_v, dtype=torch.int64, device=rowptr.device)
+        slot[perm] = torch.arange(n_v, device=rowptr.device)
+        slot = slot.to(i32).contiguous()
     return HubPlan(n_hub, n_v, seg, hub_rows.to(i32).contiguous(), vptr.to(i32).contiguous(),
-                   torch.cat([hub_rows[vhub], rest]).to(i32).contiguous(),
+                   torch.cat([vrow, rest]).to(i32).contiguous(),
                    torch.cat([vb, rp[rest]]).to(i32).contiguous(),
-                   torch.cat([ve, rp[rest + 1]]).to(i32).contiguous())
+                   torch.cat([ve, rp[rest + 1]]).to(i32).contiguous(), slot)
 
 
 class SchedCSR(NamedTuple):

@@ -299,9 +299,10 @@ def _edge_hubs(lib, csr: CSRGraph, wh_ptr: int, ld_wh: int, n_table: int, slices
         float(negative_slope), p_acc, p_ml, 0, nv, bias.data_ptr(), out.data_ptr(), hint, stream)
     if rc:
         _lib.check(rc, "gat_edge_aggregate_seg (hub split)")
-    rc = lib.gat_edge_merge(hubs.hub_rows.data_ptr(), hubs.hub_vptr.data_ptr(), hubs.n_hub,
-                            p_acc, p_ml, heads, f, int(concat), bias.data_ptr(), out.data_ptr(),
-                            0, 0, stream)
+    slot = 0 if hubs.seg_slot is None else hubs.seg_slot.data_ptr()
+    rc = lib.gat_edge_merge_ex(hubs.hub_rows.data_ptr(), hubs.hub_vptr.data_ptr(), slot,
+                               hubs.n_hub, p_acc, p_ml, heads, f, int(concat), bias.data_ptr(),
+                               out.data_ptr(), 0, 0, stream)
     if rc:
         _lib.check(rc, "gat_edge_merge")
 

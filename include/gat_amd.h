@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 8
+#define GAT_ABI_VERSION 9
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -252,6 +252,19 @@ int gat_edge_aggregate_seg(const int* seg_begin, const int* seg_end, int seg_by_
 int gat_edge_merge(const int* hub_rows, const int* seg_ptr, int n_hub, const float* st_acc,
                    const float* st_ml, int heads, int f, int concat, const float* bias,
                    float* out, float* lse, float* y_heads, void* stream);
+
+/*
+ * gat_edge_merge_ex (ABI 9): as gat_edge_merge, with the segment states
+ * addressed through seg_slot [seg_ptr[n_hub]] (segment j of the hub order at
+ * state row seg_slot[j]; NULL: j itself).  For schedules that do not run a
+ * hub's segments at adjacent positions (segments ordered by source range, so
+ * that concurrently running segments gather from the same part of the
+ * table).  The segments are combined in seg_ptr order either way, so the
+ * output does not depend on the schedule.
+ */
+int gat_edge_merge_ex(const int* hub_rows, const int* seg_ptr, const int* seg_slot, int n_hub,
+                      const float* st_acc, const float* st_ml, int heads, int f, int concat,
+                      const float* bias, float* out, float* lse, float* y_heads, void* stream);
 
 /*
  * The eval forward in one call: gat_project (slices == 1: row-major Wh at

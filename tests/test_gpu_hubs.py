@@ -87,6 +87,39 @@ def test_split_hubs_match_oracle(H, F, concat, slices, monkeypatch):
     csr_cache.clear()
 
 
+@pytest.mark.parametrize("order", [{"GAT_HUB_ORDER": "src"}, {"GAT_ROW_ORDER": "asc"},
+                                   {"GAT_HUB_ORDER": "src", "GAT_ROW_ORDER": "asc"}])
+def test_hub_schedule_orders_bitwise(order, monkeypatch):
+    """Hub segments scheduled by source range (gat_edge_merge_ex's seg_slot)
+    and whole rows by ascending degree: every segment and row computes as
+    before and the merge combines a hub's segments in the same order, so the
+    output is bitwise the default schedule's."""
+    from atmlgraphattentionnetworks_amd import tuning
+    from atmlgraphattentionnetworks_amd.graph import csr_cache, get_csr
+    monkeypatch.setenv("GAT_HUB_SEG", "64")
+    x, ei, state = _hub_case(1500, 30000, [(3, 5000), (700, 1200), (9, 300), (1499, 129),
+                                           (0, 2048)], 24, 8, 8, True, seed=7)
+    layer = _layer(state, 24, 8, 8, True)
+    outs = []
+    for env in ({}, order):
+        for k in ("GAT_HUB_ORDER", "GAT_ROW_ORDER"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        tuning.reload()
+        csr_cache.clear()
+        eid = ei.to(DEV)
+        csr = get_csr(eid, 1500)
+        assert csr.hubs is not None
+        assert (csr.hubs.seg_slot is not None) == ("GAT_HUB_ORDER" in env)
+        with torch.no_grad():
+            outs.append(layer(x.to(DEV), eid).cpu())
+    csr_cache.clear()
+    assert torch.equal(outs[0], outs[1])
+    ref = gat_layer_forward_from_state(state, x, ei, 8, True)
+    torch.testing.assert_close(outs[1], ref, atol=ATOL, rtol=RTOL)
+
+
 def test_hub_row_of_120k_edges():
     """One target with 120,000 in-edges (SURVEY §8d's power-law tail at Reddit
     scale) among uniform rows, at the default segment length: the split path
@@ -159,6 +192,8 @@ def test_edge_merge_abi_guards():
     assert lib.gat_edge_merge(0, 0, 0, 0, 0, 8, 8, 1, 0, 0, 0, 0, 0) == _lib.GAT_OK
     assert lib.gat_edge_merge(0, 0, 3, 0, 0, 8, 8, 1, 0, 0, 0, 0, 0) == _lib.GAT_EINVAL
     assert lib.gat_edge_merge(0, 0, 1, 0, 0, 65, 4, 1, 0, 0, 0, 0, 0) == _lib.GAT_EUNSUPPORTED
+    assert lib.gat_edge_merge_ex(0, 0, 0, 0, 0, 0, 8, 8, 1, 0, 0, 0, 0, 0) == _lib.GAT_OK
+    assert lib.gat_edge_merge_ex(0, 0, 0, 3, 0, 0, 8, 8, 1, 0, 0, 0, 0, 0) == _lib.GAT_EINVAL
     # store_rows needs schedule-position indexing and a state buffer
     assert lib.gat_edge_aggregate_seg(1, 1, 0, 0, 0, 0, 1, 0, 64, 1, 1, 1, 1, 0, 8, 8, 1,
                                       0.2, 0, 0, 0, 5, 0, 0, 0, 0) == _lib.GAT_EINVAL

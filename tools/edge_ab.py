@@ -29,7 +29,8 @@ KNOBS = ("GAT_EDGE_R", "GAT_EDGE_U", "GAT_EDGE_V", "GAT_EDGE_PIPE", "GAT_EDGE_LD
          "GAT_WH_SLICES", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_ORDER", "GAT_PROJ_X3",
          "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_PROJ_BM",
          "GAT_PROJ_WRES", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WRES_NW", "GAT_STORE_WT",
-         "GAT_EDGE_SCHED", "GAT_EDGE_SPLIT", "GAT_EDGE_LDSDMA", "GAT_PROJ_WG", "GAT_PROJ_X3V")
+         "GAT_EDGE_SCHED", "GAT_EDGE_SPLIT", "GAT_EDGE_LDSDMA", "GAT_PROJ_WG", "GAT_PROJ_X3V",
+         "GAT_HUB_ORDER", "GAT_ROW_ORDER", "GAT_PROJ_PRESPLIT")
 
 
 def parse(spec):
@@ -166,12 +167,13 @@ def main():
 
     class HubSeg:
         """The default plan over a copy of the CSR whose hub rows are split at
-        a different segment length (graph.hub_plan(seg_len=...))."""
+        a different segment length (graph.hub_plan(seg_len=...)) and the
+        variant's GAT_HUB_ORDER / GAT_ROW_ORDER."""
 
         def __init__(self, seg_len):
             from atmlgraphattentionnetworks_amd.graph import hub_plan
             self.csr = csr._replace(
-                hubs=hub_plan(csr.rowptr, csr.order, csr.num_edges, seg_len=seg_len))
+                hubs=hub_plan(csr.rowptr, csr.order, csr.num_edges, seg_len=seg_len, col=csr.col))
             self.plan = ForwardPlan(x, self.csr, w.heads, w.out_channels, w.concat, 0.2)
             self.plan.project(lib, x, pp)
             self.seg_len = seg_len
