@@ -3,6 +3,8 @@
 
 #include "gat_common.h"
 
+#include <utility>
+
 namespace {
 
 // ---------------------------------------------------------------------------
@@ -510,6 +512,162 @@ __global__ __launch_bounds__(256) void k_bwd_sources(
 }
 
 // ---------------------------------------------------------------------------
+// Pass 2, straight-line form for HF = 64 with 16 lanes per source row (every
+// lane one float4 of one head: the reference's training configurations 8x8
+// and 4x16).  The same arithmetic in the same order as k_bwd_sources, so the
+// results are bitwise equal, but:
+//  - the head's lane count HL = F/4 and dropout are template parameters, so
+//    the edge loop has no branches, and every load is unconditional (in
+//    k_bwd_sources the guarded loads and the runtime head-sum width split a
+//    chunk into ~80 basic blocks, and the waitcnt pass, unable to count the
+//    loads in flight across them, made each chunk wait for the id prefetch
+//    it had just issued: a full memory latency per 16 edges);
+//  - a chunk's target ids go to the row's lanes by DPP row_newbcast (a VALU
+//    modifier) instead of ds_bpermute round trips through the LDS unit;
+//  - the chunk's table gathers are issued before the next chunk's id loads
+//    (sched_barrier), so the next chunk's wait covers only loads a chunk old.
+// ---------------------------------------------------------------------------
+template <int K>
+__device__ __forceinline__ int row_bcast(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xF, 0xF, false);
+}
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>), in order
+template <class Fn, int... Is>
+__device__ __forceinline__ void static_for_impl(Fn&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int U, int HL, bool DROP>
+__global__ __launch_bounds__(256) void k_bwd_sources_sl(
+    const int* __restrict__ csc_ptr, const int* __restrict__ csc_dst,
+    const int* __restrict__ csc_eid, int n, const float* __restrict__ Wh, int ld_wh,
+    const float* __restrict__ T, int ld_t, const float* __restrict__ ds_dst,
+    const float* __restrict__ a_src, const float* __restrict__ c_src,
+    const float* __restrict__ a_dst, int H, int F, int HF, int concat, float slope,
+    DropArgs drop_arg, float* __restrict__ dwh, int ld_dwh, float* __restrict__ part) {
+    constexpr int G = 16;
+    static_assert(U == 8 || U == 16, "one id per lane per chunk");
+    const DropArgs drop = resolve_drop(drop_arg);
+    const int lane = threadIdx.x & 63;
+    const int c = lane & (G - 1);
+    const int groups = (gridDim.x * blockDim.x) / G;
+    const int gid = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / G);
+    const int coff = 4 * c;  // HF == 64: every lane holds a float4
+    const int h = c / HL;    // coff / F
+    const bool leader = c % HL == 0;
+    const int ldg = concat ? HF : F;
+    const int toff = round_up4(ldg) + 4 * h;
+    const int goff = concat ? coff : 4 * (c % HL);  // (coff % F)
+    const bool g_ok = concat || coff < F;
+    const float gs = concat ? 1.f : 1.f / (float)H;
+    const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(a_src + coff);
+    const f32x4 a2 = *reinterpret_cast<const f32x4*>(a_dst + coff);
+    const float c1 = c_src[h];
+    const auto rs_dst = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(csc_dst), (short)0,
+                                                          0x7FFFFFFF, 0x00020000);
+    const auto rs_eid = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int*>(DROP ? csc_eid : csc_dst), (short)0, 0x7FFFFFFF, 0x00020000);
+    f32x4 pa1 = zero4, pa2 = zero4, pdb = zero4, pbias = zero4;
+    float pc1 = 0.f, pc2 = 0.f;
+    for (int j = gid; j < n; j += groups) {
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(Wh + (size_t)j * ld_wh + coff);
+        const float ssrc = group_sum16(w4.x * a1.x + w4.y * a1.y + w4.z * a1.z + w4.w * a1.w, HL) + c1;
+        const int b0 = csc_ptr[j], b1 = csc_ptr[j + 1];
+        f32x4 acc = zero4;
+        float dss = 0.f;
+        int iv, kv = 0;
+        {
+            const int bb = max(min(b0 + c, b1 - 1), 0);
+            iv = csc_dst[bb];
+            if constexpr (DROP) kv = csc_eid[bb];
+        }
+        for (int b = b0; b < b1; b += U) {
+            const int nb = min(U, b1 - b);
+            f32x4 gv[U], tv[U];
+            static_for<U>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                const float* tr = T + (size_t)row_bcast<u>(iv) * ld_t;
+                gv[u] = *reinterpret_cast<const f32x4*>(tr + goff);
+                tv[u] = *reinterpret_cast<const f32x4*>(tr + toff);
+            });
+            const int kc = kv;
+            __builtin_amdgcn_sched_barrier(0);
+            {  // the next chunk's ids (past the row: its last edge again, unused).
+               // Buffer loads: a phi of this load and the row's first (a plain
+               // load) would be folded into one load at the loop top, which
+               // undoes the prefetch (byte offsets < 2^31: checked at launch)
+                const int bb = min(b + U + c, b1 - 1);
+                iv = (int)__builtin_amdgcn_raw_buffer_load_b32(rs_dst, bb * 4, 0, 0);
+                if constexpr (DROP) kv = (int)__builtin_amdgcn_raw_buffer_load_b32(rs_eid, bb * 4, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // (the arithmetic below stays after them)
+            float da[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                da[u] = group_sum16(gv[u].x * w4.x + gv[u].y * w4.y + gv[u].z * w4.z + gv[u].w * w4.w, HL);
+            static_for<U>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
+                const float z = tv[u].x + ssrc;
+                const float a = __builtin_amdgcn_exp2f((fmaxf(z, z * slope) - tv[u].y) * kLog2e);
+                float dm = 1.f;
+                if constexpr (DROP) dm = drop_factor(drop, row_bcast<u>(kc), h, H);
+                const float de = a * (dm * da[u] * gs - tv[u].z);
+                const float dz = z > 0.f ? de : de * slope;
+                const float w = u < nb ? a * dm : 0.f;
+                acc += w * gv[u];
+                dss += u < nb ? dz : 0.f;
+            });
+        }
+        const float dsd = ds_dst[(size_t)j * H + h];
+        const f32x4 d = acc * gs + dss * a1 + dsd * a2;
+        *reinterpret_cast<f32x4*>(dwh + (size_t)j * ld_dwh + coff) = d;
+        pa1 += dss * w4;
+        pa2 += dsd * w4;
+        pdb += d;
+        if (g_ok) pbias += *reinterpret_cast<const f32x4*>(T + (size_t)j * ld_t + goff);
+        if (leader) {
+            pc1 += dss;
+            pc2 += dsd;
+        }
+    }
+#pragma unroll
+    for (int off = G; off < kWave; off <<= 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            pa1[q] += __shfl_xor(pa1[q], off);
+            pa2[q] += __shfl_xor(pa2[q], off);
+            pdb[q] += __shfl_xor(pdb[q], off);
+            pbias[q] += __shfl_xor(pbias[q], off);
+        }
+        pc1 += __shfl_xor(pc1, off);
+        pc2 += __shfl_xor(pc2, off);
+    }
+    if (lane >= G) return;
+    const int wave = (int)((blockIdx.x * (size_t)blockDim.x + threadIdx.x) / kWave);
+    float* pw = part + (size_t)wave * (3 * HF + 2 * H + ldg);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        pw[coff + q] = pa1[q];
+        pw[HF + coff + q] = pa2[q];
+        pw[2 * HF + 2 * H + coff + q] = pdb[q];
+    }
+    if (g_ok) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pw[3 * HF + 2 * H + goff + q] = pbias[q];
+    }
+    if (leader) {
+        pw[2 * HF + h] = pc1;
+        pw[2 * HF + H + h] = pc2;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Backward, pass 2: one wave per SOURCE row j (CSC, grid-stride), lanes over
 // the HF columns (CQ per lane).  Over j's out-edges (target i, slot c):
 //   dWh[j]    = sum_c A[c,h] * dy[i]_h            (message backward)
@@ -995,6 +1153,32 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
         else if (u == 16) { GAT_BS(G, 16); } \
         else { GAT_BS(G, 8); }           \
         break;
+    // the straight-line kernel for HF = 64 (GAT_BWD_SL=0, A/B knob: k_bwd_sources)
+    // (its id prefetch takes buffer loads of 31-bit byte offsets: E' < 2^29,
+    // judged from the edges-per-row hint, floor(E'/N))
+    const long long hint = edges_per_row_hint & ~GAT_HINT_LOCAL;
+    bool sl = hf == 64 && (u == 8 || u == 16) && (f == 4 || f == 8 || f == 16) && hint > 0 &&
+              (hint + 1) * (long long)num_nodes < (1LL << 29);
+    if (const char* v = knob("GAT_BWD_SL")) sl = sl && std::atoi(v) != 0;
+    if (sl) {
+        const bool dr = drop.thresh != 0u;
+#define GAT_BSL(UU, HLV, DR)                                                                   \
+    hipLaunchKernelGGL((k_bwd_sources_sl<UU, HLV, DR>), grid, block, bwd_lds, st, csc_ptr, csc_dst, \
+                       csc_eid, num_nodes, wh, ld_wh, table, ld_t, ds_dst, a_src, c_src, a_dst,   \
+                       heads, f, hf, concat, negative_slope, drop, dwh, ld_dwh, partials)
+#define GAT_BSL_HL(UU, HLV) \
+    if (dr) { GAT_BSL(UU, HLV, true); } else { GAT_BSL(UU, HLV, false); }
+#define GAT_BSL_U(UU)                                   \
+    if (f == 4) { GAT_BSL_HL(UU, 1) }                    \
+    else if (f == 8) { GAT_BSL_HL(UU, 2) }               \
+    else { GAT_BSL_HL(UU, 4) }
+        if (u == 16) { GAT_BSL_U(16) }
+        else { GAT_BSL_U(8) }
+#undef GAT_BSL_U
+#undef GAT_BSL_HL
+#undef GAT_BSL
+        return status_of(hipGetLastError());
+    }
     switch (g) {
         GAT_BS_U(1) GAT_BS_U(2) GAT_BS_U(4) GAT_BS_U(8) GAT_BS_U(16) GAT_BS_U(32) GAT_BS_U(64)
         default: return GAT_EUNSUPPORTED;

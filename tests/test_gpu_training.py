@@ -173,6 +173,31 @@ def test_kink_sums_backward_equals_edge_pass(shape, p, monkeypatch):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()) + 1e-7)
 
 
+@pytest.mark.parametrize("p", [0.0, 0.6])
+@pytest.mark.parametrize("hfc", [(8, 8, True), (8, 8, False), (4, 16, True), (16, 4, False)],
+                         ids=["H8F8_cat", "H8F8_mean", "H4F16_cat", "H16F4_mean"])
+@pytest.mark.parametrize("u", ["8", "16"])
+def test_source_pass_straight_line_bitwise(hfc, p, u, monkeypatch):
+    """k_bwd_sources_sl (HF = 64, the default at 8 or 16 edges per chunk) runs
+    the same arithmetic in the same order as k_bwd_sources (GAT_BWD_SL=0):
+    every gradient bitwise equal, and both meet the float64 oracle."""
+    H, F, concat = hfc
+    monkeypatch.setenv("GAT_BWD_U", u)
+    n, e, fin = 900, 14000, 40
+    layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat, seed=21)
+    seed = 0xBEEF
+    drop = torch.from_numpy(dropout_factors(csr_positions(ei, n), H, p, seed)) if p else None
+    gout = torch.randn(n, H * F if concat else F, generator=torch.Generator().manual_seed(9))
+    res = {}
+    for sl in ("1", "0"):
+        monkeypatch.setenv("GAT_BWD_SL", sl)
+        xd, out = _run(layer, x, ei, p, seed)
+        _check_grads(layer, state, xd, out, ei, x, H, concat, gout, drop)
+        res[sl] = [xd.grad.clone()] + [q.grad.clone() for q in layer.parameters()]
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.equal(a, b)
+
+
 def test_kink_sums_used_for_hf64():
     """The default training forward at HF = 64 takes the kink-sum kernel (no
     edge pass in the backward); other head widths fall back to the edge pass."""

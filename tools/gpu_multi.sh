@@ -2,7 +2,8 @@
 # Several measurement steps in one GPU call, each under its own time limit,
 # stopping at the first failure.  Steps are given as arguments:
 #   test:<pytest -k expr>   proj:<shapes>|<variants>   emu:<workload>|<ranks>|<variants>
-#   bench:<bench.py args>   edge:<workload>|<variants>
+#   bench:<bench.py args>   edge:<workload>|<variants>   train:<workload>|<variants>|<dropout>
+#   trainstats:<workload>|<steps>   trainsq:<workload>|<steps>
 # usage: bash tools/gpu_multi.sh <tag> <step> [<step> ...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -56,6 +57,16 @@ for STEP in "$@"; do
       done
       python3 tools/pmc_edge_summary.py ${OUT}_pmc_v* > $OUT.pmc.json 2>&1; cat $OUT.pmc.json
       python3 tools/sq_summary.py ${OUT}_sq_v* > $OUT.sq.txt 2>&1; cat $OUT.sq.txt ;;
+    train)
+      # training-step A/B (tools/train_ab.py): <workload>|<variants>|<dropout>
+      W=${ARG%%|*}; REST=${ARG#*|}; V=${REST%%|*}; D=${REST#*|}
+      timeout -k 10 900 python3 -u tools/train_ab.py --workload $W --variants "$V" --dropout $D > $OUT.json 2> $OUT.err || { echo "FAILED"; tail -20 $OUT.err; exit 1; }
+      cat $OUT.json ;;
+    trainstats)
+      # kernel-trace stats of training steps (tools/train_probe.py <workload> <steps>)
+      W=${ARG%%|*}; N=${ARG#*|}
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d ${OUT}_kt -o run -- python3 tools/train_probe.py $W $N > $OUT.log 2>&1 || { echo "FAILED"; tail -20 $OUT.log; exit 1; }
+      find ${OUT}_kt -name '*kernel_stats.csv' -exec head -12 {} \; ;;
     trainsq)
       # SQ / TCP / TCC counters over a training step (tools/train_probe.py)
       W=${ARG%%|*}; N=${ARG#*|}
