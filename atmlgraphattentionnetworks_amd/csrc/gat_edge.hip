@@ -4,6 +4,8 @@
 
 #include "gat_common.h"
 
+#include <type_traits>
+
 namespace {
 
 // ---------------------------------------------------------------------------
@@ -211,7 +213,11 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 // hub merge, in registers).  The chain of dependent chunk loads per row is S
 // times shorter and a launch has S times the waves.  Only group 0 stores.
 // Not with KINK or PIPE.
-template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1>
+// HL (> 0): the head's lane count F/4V as a constant (the launcher
+// instantiates it for the HF = 64 lane groups), so the per-edge score sums
+// compile without branches; 0: read from F at run time.
+template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1,
+          int HL = 0>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -336,7 +342,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 }
                 s[u] = d2.x + d2.y;
             }
-            const int hl = F / (4 * V);  // lanes per head
+            const int hl = HL > 0 ? HL : F / (4 * V);  // lanes per head
             if (hl > 1) {
                 if (hl <= 16) {  // the head's lanes sit in one 16-lane DPP row
 #pragma unroll
@@ -379,17 +385,23 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 for (int q = 0; q < V; ++q) qq[q] += pq * v[u][q];
             }
         };
-        if (!kahan) {
+        // (dropout is kernel-uniform: one branch per chunk, not one per edge)
+        auto plain = [&](auto drc) {
+            constexpr bool DR = decltype(drc)::value;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
                 l += p;  // the softmax denominator never sees the dropout
                 float pa = p;
-                if (dropping) pa = p * drop_factor(drop, k + u, h, H);
+                if constexpr (DR) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
                 for (int q = 0; q < V; ++q) acc[q] += pa * v[u][q];
                 kink(u, p, pa, racc, accq);
             }
+        };
+        if (!kahan) {
+            if (dropping) plain(std::true_type{});
+            else plain(std::false_type{});
         } else {
             lc *= scale;
 #pragma unroll
@@ -403,16 +415,21 @@ __global__ __launch_bounds__(256) void k_edge_grp(
 #pragma unroll
                 for (int q = 0; q < V; ++q) cmpq[q] *= scale;
             }
+            auto chunk_sums = [&](auto drc) {
+                constexpr bool DR = decltype(drc)::value;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
-                ls += p;
-                float pa = p;
-                if (dropping) pa = p * drop_factor(drop, k + u, h, H);
+                for (int u = 0; u < U; ++u) {
+                    const float p = __builtin_amdgcn_exp2f(s[u] - m_new);
+                    ls += p;
+                    float pa = p;
+                    if constexpr (DR) pa = p * drop_factor(drop, k + u, h, H);
 #pragma unroll
-                for (int q = 0; q < V; ++q) cs[q] += pa * v[u][q];
-                kink(u, p, pa, rs, qs);
-            }
+                    for (int q = 0; q < V; ++q) cs[q] += pa * v[u][q];
+                    kink(u, p, pa, rs, qs);
+                }
+            };
+            if (dropping) chunk_sums(std::true_type{});
+            else chunk_sums(std::false_type{});
             // Kahan: add the chunk sums into the running sums
             auto kahan_add = [](float& sum, float& c, float part) {
                 const float y = part - c;
@@ -438,30 +455,33 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         m = m_new;
     };
     if constexpr (PIPE) {
-        // gathers software-pipelined one chunk ahead too: chunk k+U's rows are
-        // in flight while chunk k is scored and accumulated (col two ahead)
-        f32x4 vc[U][V];
-        float sc[U];
-        fetch(cv, vc, sc);
-        int cn[CL];
+        // gathers software-pipelined one chunk ahead: chunk k+U's rows are in
+        // flight while chunk k is scored and accumulated.  Two register sets
+        // (A, B) in a loop unrolled by two chunks, so no buffer is copied (a
+        // copy of the prefetched rows waits for them: the pipelining would be
+        // lost), and every fetch is unconditional (past the row's end the
+        // clamped ids repeat its last edge: gathered, unused; a conditional
+        // fetch leaves the waitcnt pass unable to count the loads in flight).
+        auto col_at = [&](int k0, int (&cc)[CL]) {
 #pragma unroll
-        for (int t = 0; t < CL; ++t) cn[t] = e1 > e0 ? col[min(e0 + U + cfirst + t * cstep, e1 - 1)] : 0;
-        for (int k = e0; k < e1; k += U) {
-            int cnn[CL];
+            for (int t = 0; t < CL; ++t) cc[t] = col[min(k0 + cfirst + t * cstep, e1 - 1)];
+        };
+        f32x4 va[U][V], vb[U][V];
+        float sa[U], sb[U];
+        int cb[CL];
+        fetch(cv, va, sa);  // (an empty row: cv = 0, row 0 gathered, unused)
 #pragma unroll
-            for (int t = 0; t < CL; ++t) cnn[t] = col[min(k + 2 * U + cfirst + t * cstep, e1 - 1)];
-            f32x4 vn[U][V];
-            float sn[U];
-            if (k + U < e1) fetch(cn, vn, sn);
-            consume(k, vc, sc);
+        for (int t = 0; t < CL; ++t) cb[t] = e1 > e0 ? col[min(e0 + U + cfirst + t * cstep, e1 - 1)] : 0;
+        for (int k = e0; k < e1; k += 2 * U) {
+            int ca2[CL], cb2[CL];
+            col_at(k + 2 * U, ca2);
+            fetch(cb, vb, sb);
+            consume(k, va, sa);
+            col_at(k + 3 * U, cb2);
+            fetch(ca2, va, sa);
+            if (k + U < e1) consume(k + U, vb, sb);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                sc[u] = sn[u];
-#pragma unroll
-                for (int q = 0; q < V; ++q) vc[u][q] = vn[u][q];
-            }
-#pragma unroll
-            for (int t = 0; t < CL; ++t) cn[t] = cnn[t];
+            for (int t = 0; t < CL; ++t) cb[t] = cb2[t];
         }
     } else {
         for (int k = e0 + half * U; k < e1; k += S * U) {
@@ -796,8 +816,29 @@ __global__ __launch_bounds__(64) void k_edge_merge(
 // Fused lane-group edge kernel, optionally with the gathers pipelined one
 // chunk ahead (GAT_EDGE_PIPE A/B knob): instantiated for the (U, V) pairs the
 // default schedule uses.
+// the fused kernel with the head's lane count hl as a constant where the
+// lane group is one of HF = 64's (G = 4, 8, 16: planes or rows, V = 1 or 2)
+// and hl is 1 or 2 (heads of 4 or 8 columns); the run-time form otherwise.
+// GAT_EDGE_HL=0 (A/B knob) forces the run-time form.
+template <int G, int U, int V, bool PIPE, bool KINK, int S, class... A>
+static void launch_grp_hl(int hl, dim3 grid, dim3 block, size_t lds, hipStream_t st, A... a) {
+    if constexpr (G == 4 || G == 8 || G == 16) {
+        const char* v = knob("GAT_EDGE_HL");
+        const bool on = v == nullptr || std::atoi(v) != 0;
+        if (on && hl == 1) {
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1>), grid, block, lds, st, a...);
+            return;
+        }
+        if (on && hl == 2) {
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 2>), grid, block, lds, st, a...);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 0>), grid, block, lds, st, a...);
+}
+
 template <int G, int U, int V, bool KINK = false, class... A>
-static void launch_edge_fused(int pipe, int split, dim3 grid, dim3 block, hipStream_t st,
+static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block, hipStream_t st,
                               A... a) {
     // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
     // kernel — caps the blocks resident per CU (160 KB / bytes)
@@ -805,9 +846,9 @@ static void launch_edge_fused(int pipe, int split, dim3 grid, dim3 block, hipStr
     if (const char* el = knob("GAT_EDGE_LDS")) lds = (size_t)std::atol(el);
     // the pipelined form is instantiated for the pair the default schedule
     // pipelines (U = 16, V = 2: Reddit-scale rows); elsewhere the knob is ignored
-    if constexpr (V == 2 && U == 16) {
+    if constexpr (V == 2 && (U == 16 || U == 8)) {
         if (pipe) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, true, KINK>), grid, block, lds, st, a...);
+            launch_grp_hl<G, U, V, true, KINK, 1>(hl, grid, block, lds, st, a...);
             return;
         }
     }
@@ -816,17 +857,15 @@ static void launch_edge_fused(int pipe, int split, dim3 grid, dim3 block, hipStr
     // row-major)
     if constexpr (!KINK && V == 1 && U <= 8 && (G == 8 || G == 16)) {
         if (split == 2) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 2>),
-                               dim3(grid.x * 2), block, lds, st, a...);
+            launch_grp_hl<G, U, V, false, false, 2>(hl, dim3(grid.x * 2), block, lds, st, a...);
             return;
         }
         if (split == 4) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 4>),
-                               dim3(grid.x * 4), block, lds, st, a...);
+            launch_grp_hl<G, U, V, false, false, 4>(hl, dim3(grid.x * 4), block, lds, st, a...);
             return;
         }
     }
-    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, KINK>), grid, block, lds, st, a...);
+    launch_grp_hl<G, U, V, false, KINK, 1>(hl, grid, block, lds, st, a...);
 }
 
 // the kink-sum forward is instantiated for the lane groups of HF = 64 heads
@@ -834,9 +873,9 @@ static void launch_edge_fused(int pipe, int split, dim3 grid, dim3 block, hipStr
 static bool kink_grp_ok(int g, int v) { return (g == 16 && v == 1) || (g == 8 && v == 2); }
 
 template <int G, int U, int V, class... A>
-static void launch_edge_kink(int pipe, dim3 grid, dim3 block, hipStream_t st, A... a) {
+static void launch_edge_kink(int pipe, int hl, dim3 grid, dim3 block, hipStream_t st, A... a) {
     if constexpr ((G == 16 && V == 1) || (G == 8 && V == 2))
-        launch_edge_fused<G, U, V, true>(pipe, 1, grid, block, st, a...);
+        launch_edge_fused<G, U, V, true>(pipe, 1, hl, grid, block, st, a...);
 }
 
 extern "C" {
@@ -987,9 +1026,9 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         slice_w, slice_stride, q_heads, r_heads, store_wt
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
     if (kink)                                                                         \
-        launch_edge_kink<G, UU, VV>(pipe, grid, block, st, GAT_GRP_KARGS);             \
+        launch_edge_kink<G, UU, VV>(pipe, hl, grid, block, st, GAT_GRP_KARGS);         \
     else if (fused)                                                                   \
-        launch_edge_fused<G, UU, VV>(pipe, split, grid, block, st, GAT_GRP_KARGS);     \
+        launch_edge_fused<G, UU, VV>(pipe, split, hl, grid, block, st, GAT_GRP_KARGS); \
     else                                                                              \
         hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, GAT_GRP_KARGS)
 #define GAT_GRP_U(G, VV)                                                              \

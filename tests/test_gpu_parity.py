@@ -33,6 +33,9 @@ VARIANTS = {
     "u16": {"GAT_EDGE_U": "16"},
     "v2_natural": {"GAT_EDGE_V": "2", "GAT_EDGE_ORDER": "natural"},
     "pipe_u16_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
+    "pipe_u8_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "8", "GAT_EDGE_V": "2"},
+    # the head's lane count read at run time instead of the HL-specialised kernels
+    "hl_runtime": {"GAT_EDGE_HL": "0"},
     "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
     "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds", "GAT_EDGE_SCHED": "0"},
     # the CSR-order launch (short rows take the scheduled copy by default)
@@ -65,7 +68,7 @@ def variant(request, monkeypatch):
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
               "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
-              "GAT_PROJ_PRESPLIT"):
+              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
