@@ -34,6 +34,7 @@ VARIANTS = {
     "v2_natural": {"GAT_EDGE_V": "2", "GAT_EDGE_ORDER": "natural"},
     "pipe_u16_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
     "pipe_u8_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "8", "GAT_EDGE_V": "2"},
+    "pipe_u4_v1": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "4", "GAT_EDGE_V": "1"},
     # the head's lane count read at run time instead of the HL-specialised kernels
     "hl_runtime": {"GAT_EDGE_HL": "0"},
     "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
