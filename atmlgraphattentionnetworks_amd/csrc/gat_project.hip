@@ -743,6 +743,20 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
     // conditional load makes the compiler's vmcnt bookkeeping assume the worst
     // at the join and wait for ALL loads in flight, the prefetch included.
     const int klast = (fin - 1) / BK * BK;  // first k of the last chunk
+    // epilogue parameters (bias, score vectors, score constants of each column
+    // tile's head), loaded before the K loop at clamped addresses: after it
+    // they were guarded loads, each waited for alone (vmcnt(0)) in every block
+    const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
+    float ep_b[NT], ep_w1[NT], ep_w2[NT], ep_c1[NT], ep_c2[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int cc = min(t * 16 + cl, HF - 1), hh = min(cc >> lf, H - 1);
+        ep_b[t] = bW[cc];
+        ep_w1[t] = a1[cc];
+        ep_w2[t] = a2[cc];
+        ep_c1[t] = c1[hh];
+        ep_c2[t] = c2[hh];
+    }
     // (sched_barrier: the two chunks' loads stay in issue order, so the oldest
     // 16 are one chunk and the stage waits for that chunk alone)
     load_chunk(0, xa_, wa_);
@@ -780,13 +794,12 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
             for (int i = 0; i < 4; ++i) acc[g][t][i] = split_sum(acc[g][t][i], cor[g][t][i]);
 
     const int hfp = round_up4(HF);
-    const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
     float* Os = xsm;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const int cc = t * 16 + cl;
-        const float bb = cc < HF ? bW[cc] : 0.f;
-        const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
+        const float bb = cc < HF ? ep_b[t] : 0.f;
+        const float w1 = cc < HF ? ep_w1[t] : 0.f, w2 = cc < HF ? ep_w2[t] : 0.f;
         const int h = cc >> lf, li = cl & (F - 1);
 #pragma unroll
         for (int g = 0; g < RG; ++g) {
@@ -804,8 +817,8 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
                 const float v2 = li == 0 ? p2[0] : li == 1 ? p2[1] : li == 2 ? p2[2] : p2[3];
                 const int rr = row0 + 16 * g + kq * 4 + li;
                 if (rr < n) {
-                    if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, v1 + c1[h], store_wt);
-                    store_out1(s_dst, (size_t)rr * H + h, v2 + c2[h], store_wt);
+                    if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, v1 + ep_c1[t], store_wt);
+                    store_out1(s_dst, (size_t)rr * H + h, v2 + ep_c2[t], store_wt);
                 }
             }
             if (F < 4 && li == 0 && h < H) {  // heads narrower than 4 lanes: rows F..3
@@ -813,8 +826,8 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
                 for (int i = 1; i < 4; ++i) {
                     const int rr = row0 + 16 * g + kq * 4 + i;
                     if (i >= F && rr < n) {
-                        if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, p1[i] + c1[h], store_wt);
-                        store_out1(s_dst, (size_t)rr * H + h, p2[i] + c2[h], store_wt);
+                        if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, p1[i] + ep_c1[t], store_wt);
+                        store_out1(s_dst, (size_t)rr * H + h, p2[i] + ep_c2[t], store_wt);
                     }
                 }
             }
