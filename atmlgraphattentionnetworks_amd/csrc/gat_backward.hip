@@ -1153,13 +1153,17 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
         else if (u == 16) { GAT_BS(G, 16); } \
         else { GAT_BS(G, 8); }           \
         break;
-    // the straight-line kernel for HF = 64 (GAT_BWD_SL=0, A/B knob: k_bwd_sources)
+    // the straight-line kernel for HF = 64: opt-in (GAT_BWD_SL=1) until it has
+    // been timed against k_bwd_sources on the GPU
     // (its id prefetch takes buffer loads of 31-bit byte offsets: E' < 2^29,
     // judged from the edges-per-row hint, floor(E'/N))
     const long long hint = edges_per_row_hint & ~GAT_HINT_LOCAL;
     bool sl = hf == 64 && (u == 8 || u == 16) && (f == 4 || f == 8 || f == 16) && hint > 0 &&
               (hint + 1) * (long long)num_nodes < (1LL << 29);
-    if (const char* v = knob("GAT_BWD_SL")) sl = sl && std::atoi(v) != 0;
+    {
+        const char* v = knob("GAT_BWD_SL");
+        sl = sl && v != nullptr && std::atoi(v) != 0;
+    }
     if (sl) {
         const bool dr = drop.thresh != 0u;
 #define GAT_BSL(UU, HLV, DR)                                                                   \

@@ -1632,12 +1632,17 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #define GAT_PIPE2_FP32(NT, LWV) (void)gp
 #endif
         // W pre-split once per call into the caller's workspace (gat_project_ex):
-        // the default x3 form then stages bf16 W tiles without splitting them
-        // (GAT_PROJ_PRESPLIT=0, A/B knob: split per workgroup as before)
+        // the x3 form then stages bf16 W tiles without splitting them.  Opt-in
+        // (GAT_PROJ_PRESPLIT=1) until it has been timed on the GPU; otherwise
+        // every workgroup splits its W tiles as before
+        // (the workspace is still accepted and sized)
         const size_t need = wsplit_bytes(hf, fin);
         bool presplit = x3 && ws != nullptr && need > 0 && ws_bytes >= need && x3v == 1 &&
                         (reinterpret_cast<uintptr_t>(ws) & 15) == 0;
-        if (const char* v = knob("GAT_PROJ_PRESPLIT")) presplit = presplit && std::atoi(v) != 0;
+        {
+            const char* v = knob("GAT_PROJ_PRESPLIT");
+            presplit = presplit && v != nullptr && std::atoi(v) != 0;
+        }
         if (presplit) {
             const int bn = nt * 16, kpad = (fin + 63) / 64 * 64;
             const int units = bn * (kpad / 8);

@@ -178,7 +178,7 @@ def test_kink_sums_backward_equals_edge_pass(shape, p, monkeypatch):
                          ids=["H8F8_cat", "H8F8_mean", "H4F16_cat", "H16F4_mean"])
 @pytest.mark.parametrize("u", ["8", "16"])
 def test_source_pass_straight_line_bitwise(hfc, p, u, monkeypatch):
-    """k_bwd_sources_sl (HF = 64, the default at 8 or 16 edges per chunk) runs
+    """k_bwd_sources_sl (HF = 64 at 8 or 16 edges per chunk, GAT_BWD_SL=1) runs
     the same arithmetic in the same order as k_bwd_sources (GAT_BWD_SL=0):
     every gradient bitwise equal, and both meet the float64 oracle."""
     H, F, concat = hfc
