@@ -65,6 +65,39 @@ def test_argument_validation_without_gpu():
         _lib.check(_lib.GAT_EUNSUPPORTED, "x")
 
 
+@pytest.mark.parametrize("fin,H,F,nbytes", [(602, 8, 8, 3 * 64 * 640 * 2), (200, 4, 8, 3 * 32 * 256 * 2),
+                                            (129, 8, 8, 3 * 64 * 192 * 2), (128, 8, 8, 0),
+                                            (50, 8, 8, 0), (602, 4, 4, 0), (602, 8, 12, 0)])
+def test_project_workspace_size(fin, H, F, nbytes):
+    """gat_project_workspace_size (ABI 8): the pre-split W planes [3][16 NT][round_up(Fin, 64)]
+    bf16 for Fin > 128 with 2 or 4 column tiles of 16 (H*F in (16, 32] or (48, 64]), else 0."""
+    from atmlgraphattentionnetworks_amd import _lib
+    assert _lib.project_workspace_bytes(fin, H, F) == nbytes
+
+
+def test_project_ex_and_merge_ex_validate_without_gpu():
+    """gat_project_ex / gat_edge_merge_ex reject bad arguments before any launch."""
+    from atmlgraphattentionnetworks_amd import _lib
+    lib = _lib.load()
+
+    def P(n, slices, ld, chunk_rows, chunk_stride, heads=8, f=8):
+        return lib.gat_project_ex(None, n, 16, None, None, None, None, None, None, heads, f, slices,
+                                  None, ld, None, heads, None, chunk_rows, chunk_stride, None, 0,
+                                  None)
+    assert P(10, 0, 64, 0, 0) == _lib.GAT_EINVAL          # no slices
+    assert P(10, 3, 64, 0, 0) == _lib.GAT_EINVAL          # 64 columns do not split in 3
+    assert P(10, 1, 64, 64, 4096) == _lib.GAT_EINVAL      # row chunks need planes
+    assert P(10, 2, 32, 64, 4096) == _lib.GAT_EINVAL      # a chunk larger than its block
+    assert P(10, 2, 64, 64, 100) == _lib.GAT_EINVAL       # chunk stride below one block
+    assert P(10, 1, 64, -1, 0) == _lib.GAT_EINVAL
+    assert lib.gat_edge_merge_ex(None, None, None, 0, None, None, 8, 8, 1, None, None, None, None,
+                                 None) == _lib.GAT_OK     # no hubs: nothing to launch
+    assert lib.gat_edge_merge_ex(None, None, None, 2, None, None, 8, 8, 1, None, None, None, None,
+                                 None) == _lib.GAT_EINVAL
+    assert lib.gat_edge_merge_ex(None, None, None, 1, None, None, 65, 4, 1, None, None, None, None,
+                                 None) == _lib.GAT_EUNSUPPORTED
+
+
 def test_csr_workspace_size():
     from atmlgraphattentionnetworks_amd import _lib
     small = _lib.csr_workspace_size(1000, 100)
