@@ -138,13 +138,15 @@ def compact_single(result: Dict, detail_path: Optional[str]) -> Dict:
             continue
         emu[wl] = {k: {"proj": v.get("max_project_ms"), "edge": v.get("max_edge_passes_ms"),
                        "compute": v.get("max_compute_ms"),
-                       "bound": v.get("compute_only_speedup_bound")}
+                       "bound": v.get("compute_only_speedup_bound"),
+                       "bound_eager": v.get("compute_only_speedup_bound_eager")}
                    for k, v in d.items() if isinstance(v, dict)}
     if emu:
         line["multi_gpu_emulated"] = emu
-        line["multi_gpu_emulated_what"] = ("per-rank ms of the node-partitioned step on one GPU, "
-                                           "max over ranks; bound = 1-GPU step / max compute "
-                                           "(collective excluded)")
+        line["multi_gpu_emulated_what"] = ("per-rank GPU ms of the node-partitioned step on one "
+                                           "GPU (graph-replayed launches), max over ranks; bound "
+                                           "= 1-GPU step / max compute (collective excluded); "
+                                           "bound_eager: the same with eager launches")
     tr = result.get("training")
     if tr:
         line["training"] = {"step_ms": tr.get("train_step_ms"),
@@ -178,7 +180,7 @@ def compact_dist(res: Dict, detail_path: Optional[str]) -> Dict:
     line["one_gpu_value"] = _get(res, "one_gpu_same_workload", "value")
     line["speedup_vs_one_gpu"] = res.get("speedup_vs_one_gpu")
     line["headline"] = phases(head)
-    line["allgather"] = phases(res.get("allgather"))
+    line["replicate"] = phases(res.get("replicate"))
     line["strategy_trials_ms"] = head.get("strategy_trials_ms")
     wls = {}
     for nm, w in (res.get("workloads") or {}).items():
@@ -186,7 +188,9 @@ def compact_dist(res: Dict, detail_path: Optional[str]) -> Dict:
                    "strategy": w.get("strategy"), "one_gpu_value": _get(w, "one_gpu", "value"),
                    "speedup": w.get("speedup_vs_one_gpu"),
                    "collective_ms": w.get("collective_ms"),
-                   "allgather": phases(w.get("allgather"))}
+                   "collective_bytes_received_per_rank":
+                       w.get("collective_bytes_received_per_rank"),
+                   "replicate": phases(w.get("replicate"))}
     line["workloads"] = wls
     weak = res.get("ppi_blocks_data_parallel")
     if weak:
@@ -194,5 +198,5 @@ def compact_dist(res: Dict, detail_path: Optional[str]) -> Dict:
                                             "ms": weak.get("ms_per_step"), "scaling": "weak"}
     line["detail"] = detail_path
     line = sig(line)
-    return fit(line, ("strategy_trials_ms", "ppi_blocks_data_parallel", "allgather",
+    return fit(line, ("strategy_trials_ms", "ppi_blocks_data_parallel", "replicate",
                       "headline", "workloads"))

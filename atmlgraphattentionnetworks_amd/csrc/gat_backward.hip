@@ -412,7 +412,7 @@ __global__ __launch_bounds__(256) void k_bwd_sources(
     for (int j = gid; j < n; j += groups) {
         const f32x4 w4 = c_ok ? *reinterpret_cast<const f32x4*>(Wh + (size_t)j * ld_wh + coff)
                               : zero4;
-        const float ssrc = hsum(w4.x * a1.x + w4.y * a1.y + w4.z * a1.z + w4.w * a1.w) + c1;
+        const float ssrc = hsum(dot4(w4, a1)) + c1;
         const int b0 = csc_ptr[j], b1 = csc_ptr[j + 1];
         f32x4 acc = zero4;
         float dss = 0.f;
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256) void k_bwd_sources(
             float da[U];
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                da[u] = hsum(gv[u].x * w4.x + gv[u].y * w4.y + gv[u].z * w4.z + gv[u].w * w4.w);
+                da[u] = hsum(dot4(gv[u], w4));
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int kpos = __shfl(kv[u / G], gbase + (u % G));
@@ -453,10 +453,10 @@ __global__ __launch_bounds__(256) void k_bwd_sources(
                 // ~10 more VALU per edge and head)
                 const float a = __builtin_amdgcn_exp2f((fmaxf(z, z * slope) - tv[u].y) * kLog2e);
                 const float dm = use_drop ? drop_factor(drop, kpos, h, H) : 1.f;
-                const float de = a * (dm * da[u] * gs - tv[u].z);
+                const float de = a * __builtin_fmaf(dm * da[u], gs, -tv[u].z);
                 const float dz = z > 0.f ? de : de * slope;
                 const float w = u < nb ? a * dm : 0.f;
-                acc += w * gv[u];
+                acc = fma4(w, gv[u], acc);
                 dss += u < nb ? dz : 0.f;
             }
 #pragma unroll
@@ -466,10 +466,10 @@ __global__ __launch_bounds__(256) void k_bwd_sources(
             }
         }
         const float dsd = ds_dst[(size_t)j * H + h];
-        const f32x4 d = acc * gs + dss * a1 + dsd * a2;
+        const f32x4 d = fma4(dsd, a2, fma4(dss, a1, acc * gs));
         if (c_ok) *reinterpret_cast<f32x4*>(dwh + (size_t)j * ld_dwh + coff) = d;
-        pa1 += dss * w4;
-        pa2 += dsd * w4;
+        pa1 = fma4(dss, w4, pa1);
+        pa2 = fma4(dsd, w4, pa2);
         pdb += c_ok ? d : zero4;
         if (g_ok) pbias += *reinterpret_cast<const f32x4*>(T + (size_t)j * ld_t + goff);
         if (leader) {
@@ -514,7 +514,8 @@ __global__ __launch_bounds__(256) void k_bwd_sources(
 // ---------------------------------------------------------------------------
 // Pass 2, straight-line form for HF = 64 with 16 lanes per source row (every
 // lane one float4 of one head: the reference's training configurations 8x8
-// and 4x16).  The same arithmetic in the same order as k_bwd_sources, so the
+// and 4x16).  The same arithmetic in the same order as k_bwd_sources (both
+// spell their fused operations out: dot4 / fma4 / fmaf, gat_common.h), so the
 // results are bitwise equal, but:
 //  - the head's lane count HL = F/4 and dropout are template parameters, so
 //    the edge loop has no branches, and every load is unconditional (in
@@ -577,7 +578,7 @@ __global__ __launch_bounds__(256) void k_bwd_sources_sl(
     float pc1 = 0.f, pc2 = 0.f;
     for (int j = gid; j < n; j += groups) {
         const f32x4 w4 = *reinterpret_cast<const f32x4*>(Wh + (size_t)j * ld_wh + coff);
-        const float ssrc = group_sum16(w4.x * a1.x + w4.y * a1.y + w4.z * a1.z + w4.w * a1.w, HL) + c1;
+        const float ssrc = group_sum16(dot4(w4, a1), HL) + c1;
         const int b0 = csc_ptr[j], b1 = csc_ptr[j + 1];
         f32x4 acc = zero4;
         float dss = 0.f;
@@ -610,25 +611,25 @@ __global__ __launch_bounds__(256) void k_bwd_sources_sl(
             float da[U];
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                da[u] = group_sum16(gv[u].x * w4.x + gv[u].y * w4.y + gv[u].z * w4.z + gv[u].w * w4.w, HL);
+                da[u] = group_sum16(dot4(gv[u], w4), HL);
             static_for<U>([&](auto uc) {
                 constexpr int u = decltype(uc)::value;
                 const float z = tv[u].x + ssrc;
                 const float a = __builtin_amdgcn_exp2f((fmaxf(z, z * slope) - tv[u].y) * kLog2e);
                 float dm = 1.f;
                 if constexpr (DROP) dm = drop_factor(drop, row_bcast<u>(kc), h, H);
-                const float de = a * (dm * da[u] * gs - tv[u].z);
+                const float de = a * __builtin_fmaf(dm * da[u], gs, -tv[u].z);
                 const float dz = z > 0.f ? de : de * slope;
                 const float w = u < nb ? a * dm : 0.f;
-                acc += w * gv[u];
+                acc = fma4(w, gv[u], acc);
                 dss += u < nb ? dz : 0.f;
             });
         }
         const float dsd = ds_dst[(size_t)j * H + h];
-        const f32x4 d = acc * gs + dss * a1 + dsd * a2;
+        const f32x4 d = fma4(dsd, a2, fma4(dss, a1, acc * gs));
         *reinterpret_cast<f32x4*>(dwh + (size_t)j * ld_dwh + coff) = d;
-        pa1 += dss * w4;
-        pa2 += dsd * w4;
+        pa1 = fma4(dss, w4, pa1);
+        pa2 = fma4(dsd, w4, pa2);
         pdb += d;
         if (g_ok) pbias += *reinterpret_cast<const f32x4*>(T + (size_t)j * ld_t + goff);
         if (leader) {

@@ -202,6 +202,25 @@ __device__ __forceinline__ float group_sum16(float v, int w) {
 }
 
 // ---------------------------------------------------------------------------
+// Explicitly fused float4 arithmetic.  With contraction left to the backend
+// (-ffp-contract=fast), an unrolled `a.x*b.x + a.y*b.y + ...` is fused
+// differently per unrolled instance once the SLP vectorizer packs some of the
+// products into v_pk_mul (fma(x, x', y*y') + z*z' + w*w' for one edge,
+// fma(w, w', fma(z, z', fma(y, y', x*x'))) for the next), so two kernels with
+// the same source expression round differently.  Kernels that promise bitwise
+// equal results to each other spell the order out with these.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float dot4(f32x4 a, f32x4 b) {
+    return __builtin_fmaf(a.w, b.w, __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)));
+}
+
+// acc + s * v, element by element, one rounding each
+__device__ __forceinline__ f32x4 fma4(float s, f32x4 v, f32x4 acc) {
+    return f32x4{__builtin_fmaf(s, v.x, acc.x), __builtin_fmaf(s, v.y, acc.y),
+                 __builtin_fmaf(s, v.z, acc.z), __builtin_fmaf(s, v.w, acc.w)};
+}
+
+// ---------------------------------------------------------------------------
 // Write-through (sc1) stores for a kernel's final outputs.  The bytes go to
 // memory as they are stored, so the kernel ends with no dirty L2 lines: the
 // dependent kernel's start does not wait for an L2 write-back of them

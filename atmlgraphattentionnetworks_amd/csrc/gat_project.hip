@@ -1614,7 +1614,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         // default for 8-B aligned rows (Reddit's 602): 64-row blocks, one chunk in
         // flight (188 registers, 2 waves per SIMD; tools/proj_bench.py: full
         // Reddit 204 -> 201 us, a P = 8 rank's 29k rows 34.4 -> 29.1 us: twice
-        // the blocks fill the CUs; profiles/r04/proj_x3v.json)
+        // the blocks fill the CUs; profiles/r04/proj_ab.json)
         int x3v = lw == 2 ? 1 : 0;
         if (const char* v = knob("GAT_PROJ_X3V")) {
             x3v = 0;

@@ -244,8 +244,11 @@ class _CSRCache:
         if device is not None and isinstance(edge_index, torch.Tensor) and \
                 edge_index.device != device:
             raise ValueError(f"edge_index is on {edge_index.device} but x is on {device}")
+        # tuning.generation: the hub / row schedule knobs are read when the CSR
+        # is built, so a tuning.reload() must not return a CSR built under the
+        # previous values (the launch plans key on it too)
         key = (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape),
-               edge_index.dtype, num_nodes, edge_index.device)
+               edge_index.dtype, num_nodes, edge_index.device, tuning.generation)
         hit = self._entries.get(key)
         if hit is not None and hit[0]() is edge_index:
             self._entries.move_to_end(key)

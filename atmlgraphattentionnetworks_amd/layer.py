@@ -416,10 +416,13 @@ class ForwardPlan:
         stream = torch._C._cuda_getCurrentRawStream(self.dev)  # the current stream, per call
         if self.pws is not None:
             ld = n if self.slices > 1 else self.hfp
+            # the sliced edge kernel recomputes s_src from the gathered row:
+            # no s_src table then (as gat_project_sliced below)
+            p_ss = self.p_ss if self.slices == 1 else 0
             rc = lib.gat_project_ex(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                     pp.a_src.data_ptr(), pp.c_src.data_ptr(),
                                     pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
-                                    self.slices, self.p_wh, ld, self.p_ss, heads, self.p_sd, 0, 0,
+                                    self.slices, self.p_wh, ld, p_ss, heads, self.p_sd, 0, 0,
                                     self.pws.data_ptr(), self.pws.numel(), stream)
             if rc == 0:
                 return

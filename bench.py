@@ -575,6 +575,8 @@ def emulated_ranks(meas: dict, ranks, exchanges=("allgather",)) -> dict:
                 kind, chunks = ("allgather", 1) if exch == "allgather_k1" else (exch, None)
                 r = emulate_rank_times(layer, csr, x, p, exchange=kind, chunks=chunks)
                 r["compute_only_speedup_bound"] = meas["ms_per_step"] / r["max_compute_ms"]
+                r["compute_only_speedup_bound_eager"] = \
+                    meas["ms_per_step"] / r["max_compute_ms_eager"]
                 r["per_rank"] = [{k: (round(v, 5) if isinstance(v, float) else v)
                                   for k, v in d.items()} for d in r["per_rank"]]
                 out[f"{exch}_P{p}"] = r

@@ -212,9 +212,11 @@ def main():
                     pp.a_src.data_ptr(), pp.c_src.data_ptr(), p.p_sd, H, F, int(w.concat), 0.2,
                     p_acc, p_ml, 0, nv, bias.data_ptr(), out.data_ptr(), p.khint, stream)
                 _lib.check(rc, "hub-last seg")
-            rc = lib.gat_edge_merge(hubs.hub_rows.data_ptr(), hubs.hub_vptr.data_ptr(), hubs.n_hub,
-                                    p_acc, p_ml, H, F, int(w.concat), bias.data_ptr(),
-                                    out.data_ptr(), 0, 0, stream)
+            # the segment slot map (GAT_HUB_ORDER=src reorders the segments)
+            slot = 0 if hubs.seg_slot is None else hubs.seg_slot.data_ptr()
+            rc = lib.gat_edge_merge_ex(hubs.hub_rows.data_ptr(), hubs.hub_vptr.data_ptr(), slot,
+                                       hubs.n_hub, p_acc, p_ml, H, F, int(w.concat),
+                                       bias.data_ptr(), out.data_ptr(), 0, 0, stream)
             _lib.check(rc, "merge")
             return out
 
