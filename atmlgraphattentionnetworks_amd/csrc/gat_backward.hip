@@ -1154,8 +1154,10 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
         else if (u == 16) { GAT_BS(G, 16); } \
         else { GAT_BS(G, 8); }           \
         break;
-    // the straight-line kernel for HF = 64: opt-in (GAT_BWD_SL=1) until it has
-    // been timed against k_bwd_sources on the GPU
+    // the straight-line kernel for HF = 64 (the default; GAT_BWD_SL=0 is the A/B
+    // knob back to k_bwd_sources): Reddit training step 8.79 -> 8.55 ms, PPI
+    // 0.568 -> 0.556 ms, same box, bitwise equal gradients
+    // (profiles/r05/train_ab_sl_*.json)
     // (its id prefetch takes buffer loads of 31-bit byte offsets: E' < 2^29,
     // judged from the edges-per-row hint, floor(E'/N))
     const long long hint = edges_per_row_hint & ~GAT_HINT_LOCAL;
@@ -1163,7 +1165,7 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
               (hint + 1) * (long long)num_nodes < (1LL << 29);
     {
         const char* v = knob("GAT_BWD_SL");
-        sl = sl && v != nullptr && std::atoi(v) != 0;
+        sl = sl && (v == nullptr || std::atoi(v) != 0);
     }
     if (sl) {
         const bool dr = drop.thresh != 0u;

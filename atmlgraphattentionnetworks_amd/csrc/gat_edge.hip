@@ -845,9 +845,11 @@ static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block
     size_t lds = 0;
     if (const char* el = knob("GAT_EDGE_LDS")) lds = (size_t)std::atol(el);
     // the pipelined form is instantiated for the pair the default schedule
-    // pipelines (U = 16, V = 2: Reddit-scale rows), U = 8 at V = 2 and the
-    // short-row chunks at V = 1 (GAT_EDGE_PIPE A/B); elsewhere the knob is ignored
-    if constexpr ((V == 2 && (U == 16 || U == 8)) || (V == 1 && U <= 8 && !KINK)) {
+    // pipelines (U = 16, V = 2: Reddit-scale rows) and U = 8 at V = 2 (GAT_EDGE_PIPE
+    // A/B); elsewhere the knob is ignored.  (Short-row chunks at V = 1 were
+    // pipelined too in round 4 and measured slower: PPI 26.9 -> 27.5 us, arxiv
+    // 54.0 -> 54.9 us, CIFAR equal; profiles/r05/edge_ab_pipe_short_*.json)
+    if constexpr (V == 2 && (U == 16 || U == 8)) {
         if (pipe) {
             launch_grp_hl<G, U, V, true, KINK, 1>(hl, grid, block, lds, st, a...);
             return;

@@ -610,41 +610,36 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
     // statically indexed)
     vec xa_[XL], xb_[PD == 2 ? XL : 1];
     wvec wa_[WQ], wb_[PD == 2 ? WQ : 1];
-    // element e = (tid + 256 q) * LW -> row e / 64, k e % 64 (coalesced rows).
-    // NTH * LW is a multiple of BK, so a thread's in-chunk k (kt) is the same for
-    // every q: per chunk one clamped k, and the row offsets (rows past n and
-    // past HF clamped: in-bounds loads that are never used) are hoisted.
-    static_assert((NTH * LW) % BK == 0, "one in-chunk k per thread");
-    const int kt = (tid * LW) % BK;
-    int xro[XL], wro[WQ];
-    bool wok[WL];
-#pragma unroll
-    for (int q = 0; q < XL; ++q) xro[q] = min(blk0 + (tid + NTH * q) * LW / BK, n - 1) * fin;
+    // element e = (tid + 256 q) * LW -> row e / 64, k e % 64 (coalesced rows);
+    // clamped, in-bounds addresses past n / fin (zeroed W meets them).  The
+    // addresses are recomputed per chunk, not hoisted into per-load registers:
+    // hoisted offsets (and epilogue parameters loaded before the loop) took
+    // Reddit's k_project_x3<4, 2, 1, 1> from 156 to 184 VGPRs, 3 -> 2 waves per
+    // SIMD, 205 -> 226 us (profiles/r05/proj_x3_ab.json)
     const int kp = (fin + BK - 1) / BK * BK;  // PS: padded K of the planes
-#pragma unroll
-    for (int q = 0; q < WQ; ++q) {
-        if constexpr (PS) {
-            // 16-B piece u of the chunk's tile: plane u / (8 BN), column
-            // (u / 8) % BN, k 8 (u % 8) .. +8 (bf16 elements)
-            const int u = tid + NTH * q;
-            wro[q] = ((u / (8 * BN)) * BN + (u / 8) % BN) * kp + 8 * (u % 8);
-        } else {
-            const int e = (tid + NTH * q) * LW;
-            wro[q] = min(e / BK, HF - 1) * fin;
-            wok[q] = e / BK < HF && e < BN * BK;  // (e past the chunk: a clamped dummy)
-        }
-    }
     auto load_chunk = [&](int k0, vec (&xn)[XL], wvec (&wn)[WQ]) {
-        const int k = min(k0 + kt, fin - LW);  // clamped past fin (the tail chunk)
 #pragma unroll
-        for (int q = 0; q < XL; ++q) xn[q] = *reinterpret_cast<const vec*>(X + xro[q] + k);
+        for (int q = 0; q < XL; ++q) {
+            const int e = (tid + NTH * q) * LW;
+            const int r = min(blk0 + e / BK, n - 1);
+            const int k = min(k0 + e % BK, fin - LW);
+            xn[q] = *reinterpret_cast<const vec*>(X + (size_t)r * fin + k);
+        }
 #pragma unroll
         for (int q = 0; q < WQ; ++q) {
-            if constexpr (PS)
+            if constexpr (PS) {
+                // 16-B piece u of the chunk's tile: plane u / (8 BN), column
+                // (u / 8) % BN, k 8 (u % 8) .. +8 (bf16 elements)
+                const int u = tid + NTH * q;
                 wn[q] = *reinterpret_cast<const u32x4*>(
-                    reinterpret_cast<const __bf16*>(W) + wro[q] + k0);
-            else
-                wn[q] = *reinterpret_cast<const vec*>(W + wro[q] + k);
+                    reinterpret_cast<const __bf16*>(W) +
+                    ((size_t)((u / (8 * BN)) * BN + (u / 8) % BN) * kp + 8 * (u % 8) + k0));
+            } else {
+                const int e = (tid + NTH * q) * LW;
+                const int nn = min(e / BK, HF - 1);  // (e past the chunk: a clamped dummy)
+                const int k = min(k0 + e % BK, fin - LW);
+                wn[q] = *reinterpret_cast<const vec*>(W + (size_t)nn * fin + k);
+            }
         }
     };
     // x chunk to LDS as fp32; W chunk split into three bf16 planes
@@ -653,7 +648,6 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
         // which must not meet the zeroed W (an infinite x would give Inf * 0 = NaN).
         // Whole chunks (block-uniform, a scalar branch) skip the selects.
         const bool full = k0 + BK <= fin;
-        const bool kin = full || k0 + kt < fin;
         if (full) {
 #pragma unroll
             for (int q = 0; q < XL; ++q) {
@@ -664,7 +658,8 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
 #pragma unroll
             for (int q = 0; q < XL; ++q) {
                 const int e = (tid + NTH * q) * LW;
-                *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) = kin ? xn[q] : vec{};
+                *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) =
+                    k0 + e % BK < fin ? xn[q] : vec{};
             }
         }
         if constexpr (PS) {
@@ -679,7 +674,7 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
 #pragma unroll
         for (int q = 0; q < WL; ++q) {
             const int e = (tid + NTH * q) * LW;
-            const bool ok = wok[q] && kin;
+            const bool ok = e / BK < HF && k0 + e % BK < fin && e < BN * BK;
             const int o = min(e / BK, BN - 1) * WSB + e % BK;
             if constexpr (LW == 1) {
                 bf16x2 p1, p2, p3;
@@ -743,20 +738,6 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
     // conditional load makes the compiler's vmcnt bookkeeping assume the worst
     // at the join and wait for ALL loads in flight, the prefetch included.
     const int klast = (fin - 1) / BK * BK;  // first k of the last chunk
-    // epilogue parameters (bias, score vectors, score constants of each column
-    // tile's head), loaded before the K loop at clamped addresses: after it
-    // they were guarded loads, each waited for alone (vmcnt(0)) in every block
-    const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
-    float ep_b[NT], ep_w1[NT], ep_w2[NT], ep_c1[NT], ep_c2[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int cc = min(t * 16 + cl, HF - 1), hh = min(cc >> lf, H - 1);
-        ep_b[t] = bW[cc];
-        ep_w1[t] = a1[cc];
-        ep_w2[t] = a2[cc];
-        ep_c1[t] = c1[hh];
-        ep_c2[t] = c2[hh];
-    }
     // (sched_barrier: the two chunks' loads stay in issue order, so the oldest
     // 16 are one chunk and the stage waits for that chunk alone)
     load_chunk(0, xa_, wa_);
@@ -794,12 +775,13 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
             for (int i = 0; i < 4; ++i) acc[g][t][i] = split_sum(acc[g][t][i], cor[g][t][i]);
 
     const int hfp = round_up4(HF);
+    const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
     float* Os = xsm;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const int cc = t * 16 + cl;
-        const float bb = cc < HF ? ep_b[t] : 0.f;
-        const float w1 = cc < HF ? ep_w1[t] : 0.f, w2 = cc < HF ? ep_w2[t] : 0.f;
+        const float bb = cc < HF ? bW[cc] : 0.f;
+        const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
         const int h = cc >> lf, li = cl & (F - 1);
 #pragma unroll
         for (int g = 0; g < RG; ++g) {
@@ -817,8 +799,8 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
                 const float v2 = li == 0 ? p2[0] : li == 1 ? p2[1] : li == 2 ? p2[2] : p2[3];
                 const int rr = row0 + 16 * g + kq * 4 + li;
                 if (rr < n) {
-                    if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, v1 + ep_c1[t], store_wt);
-                    store_out1(s_dst, (size_t)rr * H + h, v2 + ep_c2[t], store_wt);
+                    if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, v1 + c1[h], store_wt);
+                    store_out1(s_dst, (size_t)rr * H + h, v2 + c2[h], store_wt);
                 }
             }
             if (F < 4 && li == 0 && h < H) {  // heads narrower than 4 lanes: rows F..3
@@ -826,8 +808,8 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
                 for (int i = 1; i < 4; ++i) {
                     const int rr = row0 + 16 * g + kq * 4 + i;
                     if (i >= F && rr < n) {
-                        if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, p1[i] + ep_c1[t], store_wt);
-                        store_out1(s_dst, (size_t)rr * H + h, p2[i] + ep_c2[t], store_wt);
+                        if (Ss != nullptr) store_out1(Ss, (size_t)rr * ld_s + h, p1[i] + c1[h], store_wt);
+                        store_out1(s_dst, (size_t)rr * H + h, p2[i] + c2[h], store_wt);
                     }
                 }
             }
@@ -1632,16 +1614,16 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #define GAT_PIPE2_FP32(NT, LWV) (void)gp
 #endif
         // W pre-split once per call into the caller's workspace (gat_project_ex):
-        // the x3 form then stages bf16 W tiles without splitting them.  Opt-in
-        // (GAT_PROJ_PRESPLIT=1) until it has been timed on the GPU; otherwise
-        // every workgroup splits its W tiles as before
-        // (the workspace is still accepted and sized)
+        // the x3 form then stages bf16 W tiles without splitting them (the
+        // default when a workspace is given; GAT_PROJ_PRESPLIT=0 is the A/B knob
+        // back to the per-workgroup split).  Reddit 200 -> 190 us, same box
+        // (profiles/r05/proj_presplit_ab.json); equal at a P = 8 rank's 29k rows
         const size_t need = wsplit_bytes(hf, fin);
         bool presplit = x3 && ws != nullptr && need > 0 && ws_bytes >= need && x3v == 1 &&
                         (reinterpret_cast<uintptr_t>(ws) & 15) == 0;
         {
             const char* v = knob("GAT_PROJ_PRESPLIT");
-            presplit = presplit && v != nullptr && std::atoi(v) != 0;
+            presplit = presplit && (v == nullptr || std::atoi(v) != 0);
         }
         if (presplit) {
             const int bn = nt * 16, kpad = (fin + 63) / 64 * 64;

@@ -158,15 +158,17 @@ def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
     vb = rp[hub_rows][vhub] + k * seg
     ve = torch.minimum(vb + seg, rp[hub_rows + 1][vhub])
     rest = o[n_hub:]
-    if tuning.get("GAT_ROW_ORDER") == "asc":  # A/B knob: whole rows by ascending degree
-        rest = rest.flip(0)
     i32 = torch.int32
     vrow = hub_rows[vhub]
     slot = None
-    if tuning.get("GAT_HUB_ORDER") == "src" and col is not None:
+    if tuning.get("GAT_HUB_ORDER") != "hub" and col is not None:
         # segments by the first source id they gather (stable): the segments
         # running together then sweep the same part of the node table, as
-        # equal-length whole rows do (ascending sources within every row)
+        # equal-length whole rows do (ascending sources within every row).
+        # Power-law Reddit edge kernel 2.289 -> 2.242 ms against the hub-by-hub
+        # order (GAT_HUB_ORDER=hub, the A/B knob); whole rows by ascending
+        # degree measured 3.26 ms and were dropped (profiles/r05/
+        # edge_ab_hub_order_powerlaw.json)
         perm = torch.sort(col[vb].to(torch.int64), stable=True).indices
         vrow, vb, ve = vrow[perm], vb[perm], ve[perm]
         slot = torch.empty(n_v, dtype=torch.int64, device=rowptr.device)

@@ -15,8 +15,8 @@ scale (configs[3]) and the CIFAR10 superpixel batch (configs[2]).
 
 N > 1 (torchrun, one process per GPU): the same PPI-shape workload as ONE
 shared graph, node-partitioned over the GPUs, the exchange inside the step
-(the RCCL all-gather of the node table, or every rank projecting all rows,
-whichever measured faster; both reported), with Reddit and arxiv scale under
+(the RCCL all-gather of the node table, at its fastest chunk count; every rank
+projecting all rows, "replicate", is reported beside it), with Reddit and arxiv scale under
 "workloads" (atmlgraphattentionnetworks_amd/distributed.py).  The N = 1 line
 carries the per-rank compute of that partitioned step at P = 2/4/8, emulated
 on its one GPU ("multi_gpu_emulated").
@@ -241,6 +241,14 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
     csr = get_csr(ei, n)
     torch.cuda.synchronize()
     csr_ms = (time.perf_counter() - t0) * 1e3
+    # the same build again: the first one in a process also pays the one-time
+    # load of the library's GPU code objects (the first launch from each of
+    # libgat_amd.so's modules) and torch's first-use allocations
+    from atmlgraphattentionnetworks_amd.graph import build_csr
+    t0 = time.perf_counter()
+    build_csr(ei, n)
+    torch.cuda.synchronize()
+    csr_warm_ms = (time.perf_counter() - t0) * 1e3
     e_prime = csr.num_edges
     lib = _lib.load()
     stream = torch.cuda.current_stream()
@@ -297,7 +305,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
         "workload": name, "N": n, "E_prime": e_prime, "Fin": w.in_channels, "H": w.heads,
         "F": w.out_channels, "concat": w.concat,
         "value": e_prime / (ms * 1e-3), "unit": "edges/s", "ms_per_step": ms, "launch": launch,
-        "csr_build_once_ms": csr_ms,
+        "csr_build_once_ms": csr_ms, "csr_build_warm_ms": csr_warm_ms,
         "edge_kernel": {
             "kernel": plan.kernel_name(), "ms": edge_ms,
             "edges_per_s": e_prime / es,
@@ -709,7 +717,8 @@ def main():
                    "parallelism": "single GPU", "launch": head["launch"]},
         "roofline": head_sum["roofline"],
         "breakdown_ms": {"project": head["projection"]["ms"], "edge": head["edge_kernel"]["ms"],
-                         "csr_build_once": head["csr_build_once_ms"]},
+                         "csr_build_once": head["csr_build_once_ms"],
+                         "csr_build_warm": head["csr_build_warm_ms"]},
         "projection": {"bound": "mfma", "kernel": head["projection"]["kernel"],
                        "mfma_dtype": head["projection"]["mfma_dtype"],
                        "achieved": head["projection"]["mfma_issued_TFLOPs"],

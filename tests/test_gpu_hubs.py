@@ -87,13 +87,11 @@ def test_split_hubs_match_oracle(H, F, concat, slices, monkeypatch):
     csr_cache.clear()
 
 
-@pytest.mark.parametrize("order", [{"GAT_HUB_ORDER": "src"}, {"GAT_ROW_ORDER": "asc"},
-                                   {"GAT_HUB_ORDER": "src", "GAT_ROW_ORDER": "asc"}])
-def test_hub_schedule_orders_bitwise(order, monkeypatch):
-    """Hub segments scheduled by source range (gat_edge_merge_ex's seg_slot)
-    and whole rows by ascending degree: every segment and row computes as
+def test_hub_schedule_orders_bitwise(monkeypatch):
+    """Hub segments scheduled by source range (the default: gat_edge_merge_ex's
+    seg_slot) and hub by hub (GAT_HUB_ORDER=hub): every segment computes as
     before and the merge combines a hub's segments in the same order, so the
-    output is bitwise the default schedule's."""
+    outputs are bitwise equal."""
     from atmlgraphattentionnetworks_amd import tuning
     from atmlgraphattentionnetworks_amd.graph import csr_cache, get_csr
     monkeypatch.setenv("GAT_HUB_SEG", "64")
@@ -101,9 +99,8 @@ def test_hub_schedule_orders_bitwise(order, monkeypatch):
                                            (0, 2048)], 24, 8, 8, True, seed=7)
     layer = _layer(state, 24, 8, 8, True)
     outs = []
-    for env in ({}, order):
-        for k in ("GAT_HUB_ORDER", "GAT_ROW_ORDER"):
-            monkeypatch.delenv(k, raising=False)
+    for env in ({"GAT_HUB_ORDER": "hub"}, {}):
+        monkeypatch.delenv("GAT_HUB_ORDER", raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         tuning.reload()
@@ -111,7 +108,7 @@ def test_hub_schedule_orders_bitwise(order, monkeypatch):
         eid = ei.to(DEV)
         csr = get_csr(eid, 1500)
         assert csr.hubs is not None
-        assert (csr.hubs.seg_slot is not None) == ("GAT_HUB_ORDER" in env)
+        assert (csr.hubs.seg_slot is None) == ("GAT_HUB_ORDER" in env)
         with torch.no_grad():
             outs.append(layer(x.to(DEV), eid).cpu())
     csr_cache.clear()

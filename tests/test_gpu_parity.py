@@ -34,7 +34,6 @@ VARIANTS = {
     "v2_natural": {"GAT_EDGE_V": "2", "GAT_EDGE_ORDER": "natural"},
     "pipe_u16_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
     "pipe_u8_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "8", "GAT_EDGE_V": "2"},
-    "pipe_u4_v1": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "4", "GAT_EDGE_V": "1"},
     # the head's lane count read at run time instead of the HL-specialised kernels
     "hl_runtime": {"GAT_EDGE_HL": "0"},
     "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
@@ -53,10 +52,11 @@ VARIANTS = {
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
     "proj_wk_lds_epilogue": {"GAT_PROJ_WK_DIRECT": "0"},
     "plain_stores": {"GAT_STORE_WT": "0"},
-    # Fin > 128: W pre-split once per launch into gat_project_ex's workspace
-    # (opt-in), also for 4-float / 1-float rows
-    "proj_presplit": {"GAT_PROJ_PRESPLIT": "1"},
-    "proj_x3_b64p1": {"GAT_PROJ_X3V": "b64p1", "GAT_PROJ_PRESPLIT": "1"},
+    # Fin > 128: W pre-split once per launch into gat_project_ex's workspace is
+    # the default; the per-workgroup split (GAT_PROJ_PRESPLIT=0), also for the
+    # 64-row one-chunk x3 form with 4-float / 1-float rows
+    "proj_no_presplit": {"GAT_PROJ_PRESPLIT": "0"},
+    "proj_x3_b64p1": {"GAT_PROJ_X3V": "b64p1"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
 }

@@ -16,9 +16,11 @@ ok() {  # continue after pass (0) or test failures (1); stop on anything else
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step rc=$rc: stopping"; exit $rc; fi
 }
 OLD=abtree/bda929d
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-  > $O/pytest_gpu.txt 2>&1; ok $?
-tail -5 $O/pytest_gpu.txt
+if [ "$1" != "--no-tests" ]; then
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > $O/pytest_gpu.txt 2>&1; ok $?
+  tail -5 $O/pytest_gpu.txt
+fi
 BARGS="--no-cpu-baseline --no-pmc --emulate-ranks 2,4,8 --no-train --workloads reddit,reddit_powerlaw,arxiv --steps 20"
 for r in 1 2; do
   (cd $OLD && timeout -k 10 300 python3 bench.py $BARGS --detail-out /tmp/old_detail.json) > $O/bench_old_$r.json 2> $O/bench_old_$r.err || exit 2
