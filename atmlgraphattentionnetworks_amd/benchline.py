@@ -169,7 +169,8 @@ def compact_dist(res: Dict, detail_path: Optional[str]) -> Dict:
     def phases(d):
         if not d:
             return None
-        return {"strategy": d.get("strategy"), "value": d.get("value"),
+        return {"strategy": d.get("strategy"), "launch": d.get("launch", "eager"),
+                "value": d.get("value"),
                 "ms": d.get("ms_per_step"), "collective_ms": d.get("collective_ms"),
                 "project_ms": d.get("project_ms_max_over_ranks"),
                 "edge_ms": d.get("edge_passes_ms_max_over_ranks"),
@@ -181,11 +182,20 @@ def compact_dist(res: Dict, detail_path: Optional[str]) -> Dict:
     line["speedup_vs_one_gpu"] = res.get("speedup_vs_one_gpu")
     line["headline"] = phases(head)
     line["replicate"] = phases(res.get("replicate"))
+
+    def graph(d):
+        g = (d or {}).get("graph")
+        if not g:
+            return None
+        return {"ok": g.get("ok"), "value": g.get("value"), "ms": g.get("ms_per_step"),
+                "eager_value": _get(d, "eager", "value"), "error": g.get("error")}
+    line["graph"] = graph(head)
     line["strategy_trials_ms"] = head.get("strategy_trials_ms")
     wls = {}
     for nm, w in (res.get("workloads") or {}).items():
         wls[nm] = {"value": w.get("value"), "ms": w.get("ms_per_step"),
-                   "strategy": w.get("strategy"), "one_gpu_value": _get(w, "one_gpu", "value"),
+                   "strategy": w.get("strategy"), "launch": w.get("launch", "eager"),
+                   "graph": graph(w), "one_gpu_value": _get(w, "one_gpu", "value"),
                    "speedup": w.get("speedup_vs_one_gpu"),
                    "collective_ms": w.get("collective_ms"),
                    "collective_bytes_received_per_rank":
