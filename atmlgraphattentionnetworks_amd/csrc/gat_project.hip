@@ -1535,7 +1535,8 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
         return status_of(hipGetLastError());
     }
     int wk_max = 64;  // GAT_PROJ_WK_MAX (A/B knob): largest fin for the whole-K kernel
-    if (const char* v = knob("GAT_PROJ_WK_MAX")) wk_max = std::atoi(v);
+    // (at most 64: its staging loads cover 64 x 64 floats of X and W)
+    if (const char* v = knob("GAT_PROJ_WK_MAX")) wk_max = std::min(std::atoi(v), 64);
     const bool wk_ok = fin > 0 && fin <= wk_max && aligned16 && wk_lds <= 160 * 1024 &&
                        (pk == nullptr || std::strcmp(pk, "wk") == 0);
     if (wk_ok) {

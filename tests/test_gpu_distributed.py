@@ -325,6 +325,15 @@ def test_bench_dist_one_rank_rccl(tmp_path):
     assert d["config"]["strategy"].startswith("allgather")
     assert head["collective_ms"] > 0
     assert head["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * head["check"]["max_abs_ref"]
+    # the same all-gather step replayed from a captured graph (the RCCL
+    # collective recorded in it): captured, timed and checked
+    g = head["graph"]
+    assert g["ok"], g
+    assert g["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * g["check"]["max_abs_ref"]
+    # the headline is the faster launch of the same strategy
+    assert d["value"] >= g["value"] * (1 - 1e-9)
+    if "eager" in head:  # the graph won
+        assert d["value"] == g["value"] and d["config"]["launch"].startswith("hipGraph")
 
 
 def test_bench_single_gpu_line(tmp_path):

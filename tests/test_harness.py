@@ -184,3 +184,26 @@ def test_compact_line_drops_optional_keys_first():
     assert "big" not in out and out["small"] == 2 and all(k in out for k in REQUIRED)
     out = fit({**line, "other": "y" * 10000}, ("big",), budget=500)
     assert "truncated" in out and all(k in out for k in REQUIRED)
+
+
+def test_compact_dist_line_keeps_allgather_headline_and_graph():
+    """The N > 1 line built from round 5's --dist detail (one-rank RCCL group,
+    graph-replayed all-gather step): under the budget, required keys kept, the
+    headline on the all-gather strategy with its launch mode, the graph trial
+    summarised and 'replicate' beside it."""
+    import json
+    import os
+    from atmlgraphattentionnetworks_amd.benchline import LINE_BUDGET, REQUIRED, compact_dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    full = json.load(open(os.path.join(root, "profiles", "r05", "bench_dist1_graph_detail.json")))
+    line = compact_dist(full, "gpurun_out/bench_detail.json")
+    assert len(json.dumps(line)) <= LINE_BUDGET
+    for k in REQUIRED:
+        assert k in line, k
+    assert line["config"]["strategy"].startswith("allgather")
+    assert line["headline"]["strategy"] == line["config"]["strategy"]
+    assert line["headline"]["launch"] == line["config"]["launch"]
+    assert line["graph"]["ok"] is True and line["graph"]["eager_value"] < line["value"]
+    assert line["replicate"]["strategy"] == "replicate"
+    arx = line["workloads"]["arxiv"]
+    assert arx["strategy"].startswith("allgather") and arx["graph"]["ok"] is True
