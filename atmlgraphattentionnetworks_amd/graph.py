@@ -119,14 +119,17 @@ def locality_hint(rowptr: torch.Tensor, col: torch.Tensor, num_nodes: int,
 
 
 def hub_segment_len(num_edges: int) -> int:
-    """Edges per hub segment: a power of two in [256, 2048], ~E'/50000 (a
+    """Edges per hub segment: a power of two in [256, 1024], ~E'/50000 (a
     segment should take a small fraction of the whole edge kernel: PPI and
-    arxiv scale 256, Reddit scale 2048).  GAT_HUB_SEG overrides."""
+    arxiv scale 256, Reddit scale 1024).  With the segments ordered by source
+    (hub_plan), power-law Reddit's edge kernel ran 2.234 / 2.154 / 2.346 /
+    2.531 ms at 2048 / 1024 / 512 / 4096 (profiles/r05/edge_ab_hubseg_powerlaw.json);
+    uniform Reddit has no row past 2 x 1024.  GAT_HUB_SEG overrides."""
     env = tuning.get("GAT_HUB_SEG")
     if env is not None:
         return max(16, int(env))
     s = 256
-    while s < 2048 and 2 * s <= num_edges // 50000:
+    while s < 1024 and 2 * s <= num_edges // 50000:
         s *= 2
     return s
 
