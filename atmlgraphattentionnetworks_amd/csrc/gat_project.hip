@@ -1043,6 +1043,173 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_project_wres with the direct epilogue (heads of 4, 8 or 16 columns), for
+// three workgroups / waves per SIMD instead of two.  k_project_wres holds two
+// per CU at arxiv's K = 128: 69.6 KB of LDS (W planes 52 KB + a 17 KB output
+// tile per wave) and 199 VGPRs; its SQ counters (profiles/r03/sq_counters_arxiv
+// .txt) show the waves 44% of their life waiting, 18% issuing VALU.  Here:
+//  - the MFMA operands are swapped (A = W fragment, B = x fragment), so a lane
+//    holds four consecutive columns of one row and the Wh float4s and the
+//    fused scores leave from registers (proj_direct_epilogue, as k_project_wk):
+//    no output tile, no LDS round trip, no wave barrier;
+//  - the epilogue parameters sit in LDS (1.3 KB), not in 20 VGPRs;
+//  - a tile's x fragments are split one k-step at a time, the next tile's loads
+//    for that k-step issued right after (12 live bf16x8 VGPRs instead of 48).
+// LDS 53.5 KB and <= 168 VGPRs: three workgroups per CU.  Same products and
+// split-sum as k_project_wres.
+// ---------------------------------------------------------------------------
+template <int NT, int LW, int KS>
+__global__ __launch_bounds__(256, 3) void k_project_wres_d(
+    const float* __restrict__ X, int n, int fin,
+    const float* __restrict__ W, const float* __restrict__ bW,
+    const float* __restrict__ a1, const float* __restrict__ c1,
+    const float* __restrict__ a2, const float* __restrict__ c2,
+    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
+    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt, int crows,
+    long long cjump) {
+    GAT_ROW_CHUNKS();
+    constexpr int BN = NT * 16, KP = KS * 32;  // padded K
+    constexpr int WSB = KP + 8;
+    constexpr int NL = 8 / LW;                  // loads per 8-float fragment
+    using vec = typename std::conditional<LW == 4, f32x4,
+                typename std::conditional<LW == 2, f32x2, float>::type>::type;
+    __shared__ __attribute__((aligned(16))) __bf16 wsb[3][BN * WSB];
+    __shared__ __attribute__((aligned(16))) float prm[3 * BN + 128];
+    float* bs = prm;
+    float* a1s = prm + BN;
+    float* a2s = prm + 2 * BN;
+    float* c1s = prm + 3 * BN;
+    float* c2s = c1s + 64;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int cl = lane & 15, kq = lane >> 4;
+    const int tiles = (n + 15) / 16;
+    const int tstride = gridDim.x * 4;
+    int tile = blockIdx.x * 4 + w;
+    vec xr[KS][NL];
+    auto load_step = [&](const float* xrow, int s) {
+#pragma unroll
+        for (int q = 0; q < NL; ++q) {
+            const int k = min(32 * s + 8 * kq + LW * q, fin - LW);
+            xr[s][q] = *reinterpret_cast<const vec*>(xrow + k);
+        }
+    };
+    {
+        const float* xrow = X + (size_t)min(min(tile, tiles - 1) * 16 + cl, n - 1) * fin;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) load_step(xrow, s);
+    }
+    if (tid < BN) {
+        const bool ok = tid < HF;
+        const int cc = ok ? tid : 0;
+        const float bv = bW[cc], av1 = a1[cc], av2 = a2[cc];
+        bs[tid] = ok ? bv : 0.f;
+        a1s[tid] = ok ? av1 : 0.f;
+        a2s[tid] = ok ? av2 : 0.f;
+    }
+    if (tid < H) {
+        const float v1 = c1[tid], v2 = c2[tid];
+        c1s[tid] = v1;
+        c2s[tid] = v2;
+    }
+    {  // W split into three bf16 planes, as k_project_wres
+        constexpr int WQ = (BN * KP + 256 * LW - 1) / (256 * LW);
+        vec wv[WQ];
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) {
+            const int e = (tid + 256 * q) * LW;
+            const int c = min(e / KP, HF - 1), k = min(e % KP, fin - LW);
+            wv[q] = *reinterpret_cast<const vec*>(W + (size_t)c * fin + k);
+        }
+#pragma unroll
+        for (int q = 0; q < WQ; ++q) {
+            const int e = (tid + 256 * q) * LW;
+            if (e < BN * KP) {
+                const int c = e / KP, k = e % KP;
+                const bool ok = c < HF && k < fin;
+                const int o = c * WSB + k;
+                if constexpr (LW == 1) {
+                    bf16x2 p1, p2, p3;
+                    split3_pair(f32x2{ok ? wv[q] : 0.f, 0.f}, p1, p2, p3);
+                    wsb[0][o] = p1[0];
+                    wsb[1][o] = p2[0];
+                    wsb[2][o] = p3[0];
+                } else if constexpr (LW == 2) {
+                    bf16x2 p1, p2, p3;
+                    split3_pair(ok ? wv[q] : f32x2{0.f, 0.f}, p1, p2, p3);
+                    *reinterpret_cast<bf16x2*>(&wsb[0][o]) = p1;
+                    *reinterpret_cast<bf16x2*>(&wsb[1][o]) = p2;
+                    *reinterpret_cast<bf16x2*>(&wsb[2][o]) = p3;
+                } else {
+                    const f32x4 v = ok ? wv[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+                    bf16x2 p1a, p2a, p3a, p1b, p2b, p3b;
+                    split3_pair(f32x2{v.x, v.y}, p1a, p2a, p3a);
+                    split3_pair(f32x2{v.z, v.w}, p1b, p2b, p3b);
+                    *reinterpret_cast<bf16x4*>(&wsb[0][o]) = bf16x4{p1a[0], p1a[1], p1b[0], p1b[1]};
+                    *reinterpret_cast<bf16x4*>(&wsb[1][o]) = bf16x4{p2a[0], p2a[1], p2b[0], p2b[1]};
+                    *reinterpret_cast<bf16x4*>(&wsb[2][o]) = bf16x4{p3a[0], p3a[1], p3b[0], p3b[1]};
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    for (; tile < tiles; tile += tstride) {
+        // the next tile's row (the last tile re-loads itself, unused: every load
+        // is unconditional, see k_project_wres)
+        const float* xnext =
+            X + (size_t)min(min(tile + tstride, tiles - 1) * 16 + cl, n - 1) * fin;
+        f32x4 acc[NT], cor[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = cor[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            bf16x8 x1, x2, x3;
+            {
+                float f[8];
+#pragma unroll
+                for (int q = 0; q < NL; ++q) {
+                    // k past fin (clamped loads of this row's real x) meets zero W
+                    const bool kin = 32 * s + 8 * kq + LW * q < fin;
+#pragma unroll
+                    for (int j = 0; j < LW; ++j) {
+                        if constexpr (LW == 1) f[q] = kin ? xr[s][q] : 0.f;
+                        else f[q * LW + j] = kin ? xr[s][q][j] : 0.f;
+                    }
+                }
+                split3_x8(f32x4{f[0], f[1], f[2], f[3]}, f32x4{f[4], f[5], f[6], f[7]}, x1, x2, x3);
+            }
+            load_step(xnext, s);  // xr[s] is free: the next tile's k-step s
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                int o = (t * 16 + cl) * WSB + 32 * s + 8 * kq;
+                // opaque per iteration: the W fragments are the same for every
+                // tile, and hoisted out of the tile loop they would hold
+                // KS x NT x 3 x 4 = 192 VGPRs at arxiv (spilled under the bound)
+                asm volatile("" : "+v"(o));
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&wsb[0][o]);
+                const bf16x8 b2 = *reinterpret_cast<const bf16x8*>(&wsb[1][o]);
+                const bf16x8 b3 = *reinterpret_cast<const bf16x8*>(&wsb[2][o]);
+                // swapped operands: the accumulator holds Wh^T (lane: row cl,
+                // columns 16t + 4kq .. +4)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x1, acc[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, x1, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x2, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b3, x1, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, x2, cor[t], 0, 0, 0);
+                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, x3, cor[t], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[t][i] = split_sum(acc[t][i], cor[t][i]);
+        proj_direct_epilogue<NT>(acc, tile * 16 + cl, n, kq, bs, a1s, a2s, c1s, c2s, H, F, HF, Wh,
+                                 ld_wh, Ss, ld_s, s_dst, slice_w, slice_stride, store_wt);
+    }
+}
+
 #ifdef GAT_AB_KERNELS  // measured and not adopted (profiles/r04/proj_ab.json); tools-only build
 // ---------------------------------------------------------------------------
 // Projection for fin in {32, 64, 128} (ogbn-arxiv's 128), split-bf16 MFMA:
@@ -1510,12 +1677,25 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
             return status_of(hipGetLastError());
         }
 #endif
+        // the direct-epilogue form (heads of 4, 8 or 16 columns): three
+        // workgroups per CU (GAT_PROJ_WRES_DIRECT A/B knob, off until timed)
+        bool wdir = false;
+        if (const char* v = knob("GAT_PROJ_WRES_DIRECT")) wdir = std::atoi(v) != 0;
+        wdir = wdir && (f == 4 || f == 8 || f == 16);
+        if (wdir) wg_cu = 3;
         const int grid_w = (int)std::max<long long>(
             1, std::min<long long>((tiles + 3) / 4, 256LL * wg_cu / ny));
 #define GAT_WRES(NTV, LWV, KSV)                                                               \
-    hipLaunchKernelGGL((k_project_wres<NTV, LWV, KSV>), dim3(grid_w, ny), dim3(256), 0, st, x, \
-                       n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh,     \
-                       s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, cjump)
+    if (wdir)                                                                                 \
+        hipLaunchKernelGGL((k_project_wres_d<NTV, LWV, KSV>), dim3(grid_w, ny), dim3(256), 0, \
+                           st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, \
+                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, \
+                           cjump);                                                            \
+    else                                                                                      \
+        hipLaunchKernelGGL((k_project_wres<NTV, LWV, KSV>), dim3(grid_w, ny), dim3(256), 0,   \
+                           st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, \
+                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, \
+                           cjump)
 #define GAT_WRES_KS(NTV, LWV)                                          \
     switch (ks) {                                                      \
         case 1: GAT_WRES(NTV, LWV, 1); break;                          \

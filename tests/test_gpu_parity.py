@@ -49,6 +49,8 @@ VARIANTS = {
     # every fin <= 128, the tiled fallback; plain stores instead of write-through
     "proj_wk": {"GAT_PROJ_WRES": "0"},
     "proj_wres": {"GAT_PROJ_WRES": "1"},
+    # k_project_wres with the direct epilogue (heads of 4, 8, 16 columns)
+    "proj_wres_direct": {"GAT_PROJ_WRES": "1", "GAT_PROJ_WRES_DIRECT": "1"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
     "proj_wk_lds_epilogue": {"GAT_PROJ_WK_DIRECT": "0"},
     "plain_stores": {"GAT_STORE_WT": "0"},
@@ -69,7 +71,7 @@ def variant(request, monkeypatch):
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
               "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
-              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL"):
+              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -436,7 +438,8 @@ def test_projection_presplit_bitwise(fin, heads, x3v, chunks, monkeypatch):
 
 
 @pytest.mark.parametrize("fin,kernel", [(50, None), (50, "tiled"), (128, None), (100, None),
-                                        (200, None), (602, None), (130, "tiled")])
+                                        (200, None), (602, None), (130, "tiled"),
+                                        (128, "wres_direct"), (100, "wres_direct")])
 def test_projection_non_finite_inputs(fin, kernel, monkeypatch):
     """Non-finite x (include/gat_amd.h, gat_project): rows without a
     non-finite value are unaffected (no leak into other rows through clamped
@@ -447,7 +450,9 @@ def test_projection_non_finite_inputs(fin, kernel, monkeypatch):
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer
     from atmlgraphattentionnetworks_amd import tuning
     from atmlgraphattentionnetworks_amd.layer import alloc_table, project
-    if kernel is not None:
+    if kernel == "wres_direct":
+        monkeypatch.setenv("GAT_PROJ_WRES_DIRECT", "1")
+    elif kernel is not None:
         monkeypatch.setenv("GAT_PROJ_KERNEL", kernel)
     tuning.reload()
     d = dev()
