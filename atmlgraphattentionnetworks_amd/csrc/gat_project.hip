@@ -1057,7 +1057,8 @@ __global__ __launch_bounds__(256, 2) void k_project_wres(
 //  - a tile's x fragments are split one k-step at a time, the next tile's loads
 //    for that k-step issued right after (12 live bf16x8 VGPRs instead of 48).
 // LDS 53.5 KB and <= 168 VGPRs: three workgroups per CU.  Same products and
-// split-sum as k_project_wres.
+// split-sum as k_project_wres (outputs within 1e-6 of it: the MFMA's operand
+// roles differ).  The default for those heads (arxiv 40.3 -> 31.7 us).
 // ---------------------------------------------------------------------------
 template <int NT, int LW, int KS>
 __global__ __launch_bounds__(256, 3) void k_project_wres_d(
@@ -1677,9 +1678,11 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
             return status_of(hipGetLastError());
         }
 #endif
-        // the direct-epilogue form (heads of 4, 8 or 16 columns): three
-        // workgroups per CU (GAT_PROJ_WRES_DIRECT A/B knob, off until timed)
-        bool wdir = false;
+        // the direct-epilogue form (heads of 4, 8 or 16 columns), three
+        // workgroups per CU: arxiv 40.3 -> 31.7 us, a P = 8 rank's 21k rows
+        // 11.4 -> 9.9 us, same box (profiles/r05/proj_wres_direct.json).
+        // GAT_PROJ_WRES_DIRECT=0 (A/B knob): k_project_wres
+        bool wdir = true;
         if (const char* v = knob("GAT_PROJ_WRES_DIRECT")) wdir = std::atoi(v) != 0;
         wdir = wdir && (f == 4 || f == 8 || f == 16);
         if (wdir) wg_cu = 3;

@@ -49,8 +49,9 @@ VARIANTS = {
     # every fin <= 128, the tiled fallback; plain stores instead of write-through
     "proj_wk": {"GAT_PROJ_WRES": "0"},
     "proj_wres": {"GAT_PROJ_WRES": "1"},
-    # k_project_wres with the direct epilogue (heads of 4, 8, 16 columns)
-    "proj_wres_direct": {"GAT_PROJ_WRES": "1", "GAT_PROJ_WRES_DIRECT": "1"},
+    # k_project_wres with its output-tile epilogue instead of the direct one
+    # (the default for heads of 4, 8, 16 columns)
+    "proj_wres_tile": {"GAT_PROJ_WRES": "1", "GAT_PROJ_WRES_DIRECT": "0"},
     "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
     "proj_wk_lds_epilogue": {"GAT_PROJ_WK_DIRECT": "0"},
     "plain_stores": {"GAT_STORE_WT": "0"},
@@ -439,7 +440,7 @@ def test_projection_presplit_bitwise(fin, heads, x3v, chunks, monkeypatch):
 
 @pytest.mark.parametrize("fin,kernel", [(50, None), (50, "tiled"), (128, None), (100, None),
                                         (200, None), (602, None), (130, "tiled"),
-                                        (128, "wres_direct"), (100, "wres_direct")])
+                                        (128, "wres_tile"), (100, "wres_tile")])
 def test_projection_non_finite_inputs(fin, kernel, monkeypatch):
     """Non-finite x (include/gat_amd.h, gat_project): rows without a
     non-finite value are unaffected (no leak into other rows through clamped
@@ -450,8 +451,8 @@ def test_projection_non_finite_inputs(fin, kernel, monkeypatch):
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer
     from atmlgraphattentionnetworks_amd import tuning
     from atmlgraphattentionnetworks_amd.layer import alloc_table, project
-    if kernel == "wres_direct":
-        monkeypatch.setenv("GAT_PROJ_WRES_DIRECT", "1")
+    if kernel == "wres_tile":
+        monkeypatch.setenv("GAT_PROJ_WRES_DIRECT", "0")
     elif kernel is not None:
         monkeypatch.setenv("GAT_PROJ_KERNEL", kernel)
     tuning.reload()
