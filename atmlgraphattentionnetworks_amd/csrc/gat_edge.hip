@@ -216,8 +216,12 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 // HL (> 0): the head's lane count F/4V as a constant (the launcher
 // instantiates it for the HF = 64 lane groups), so the per-edge score sums
 // compile without branches; 0: read from F at run time.
+// LEAN: the eval forward over rows all shorter than 1024 edges (the caller's
+// GAT_HINT_SHORT_ROWS, no dropout): no compensated-sum and no dropout code,
+// whose registers every row otherwise pays for (PPI's short-row instance:
+// 76 -> 60 VGPRs, 6 -> 8 waves per SIMD).
 template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1,
-          int HL = 0>
+          int HL = 0, bool LEAN = false>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -270,8 +274,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     }
     const int si = er.by_pos ? pos : r;  // segment / state index
     const int e0 = er.eb[si], e1 = er.ee[si];
-    const bool kahan = e1 - e0 >= 1024;
-    const bool dropping = drop.thresh != 0u;  // kernel-uniform: a scalar branch
+    const bool kahan = !LEAN && e1 - e0 >= 1024;
+    const bool dropping = !LEAN && drop.thresh != 0u;  // kernel-uniform: a scalar branch
     // the target's share of every score, in log2 units (LeakyReLU is positively
     // homogeneous: LReLU(z) log2e = LReLU(z log2e)); + c1 when s_src is recomputed
     const float sd = (s_dst[(size_t)r * H + h] + c1) * kLog2e;
@@ -821,10 +825,25 @@ __global__ __launch_bounds__(64) void k_edge_merge(
 // and hl is 1 or 2 (heads of 4 or 8 columns); the run-time form otherwise.
 // GAT_EDGE_HL=0 (A/B knob) forces the run-time form.
 template <int G, int U, int V, bool PIPE, bool KINK, int S, class... A>
-static void launch_grp_hl(int hl, dim3 grid, dim3 block, size_t lds, hipStream_t st, A... a) {
+static void launch_grp_hl(int hl, bool lean, dim3 grid, dim3 block, size_t lds, hipStream_t st,
+                          A... a) {
     if constexpr (G == 4 || G == 8 || G == 16) {
         const char* v = knob("GAT_EDGE_HL");
         const bool on = v == nullptr || std::atoi(v) != 0;
+        // the lean eval instance (LEAN): the short-row schedules (V = 1, U = 4
+        // or 8, one lane group per row) of HF = 64's heads
+        if constexpr (V == 1 && (U == 4 || U == 8) && !PIPE && !KINK && S == 1) {
+            if (on && lean && hl == 1) {
+                hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 1, 1, true>), grid,
+                                   block, lds, st, a...);
+                return;
+            }
+            if (on && lean && hl == 2) {
+                hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 1, 2, true>), grid,
+                                   block, lds, st, a...);
+                return;
+            }
+        }
         if (on && hl == 1) {
             hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1>), grid, block, lds, st, a...);
             return;
@@ -838,8 +857,8 @@ static void launch_grp_hl(int hl, dim3 grid, dim3 block, size_t lds, hipStream_t
 }
 
 template <int G, int U, int V, bool KINK = false, class... A>
-static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block, hipStream_t st,
-                              A... a) {
+static void launch_edge_fused(int pipe, int split, int hl, bool lean, dim3 grid, dim3 block,
+                              hipStream_t st, A... a) {
     // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
     // kernel — caps the blocks resident per CU (160 KB / bytes)
     size_t lds = 0;
@@ -851,7 +870,7 @@ static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block
     // 54.0 -> 54.9 us, CIFAR equal; profiles/r05/edge_ab_pipe_short_*.json)
     if constexpr (V == 2 && (U == 16 || U == 8)) {
         if (pipe) {
-            launch_grp_hl<G, U, V, true, KINK, 1>(hl, grid, block, lds, st, a...);
+            launch_grp_hl<G, U, V, true, KINK, 1>(hl, false, grid, block, lds, st, a...);
             return;
         }
     }
@@ -860,15 +879,17 @@ static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block
     // row-major)
     if constexpr (!KINK && V == 1 && U <= 8 && (G == 8 || G == 16)) {
         if (split == 2) {
-            launch_grp_hl<G, U, V, false, false, 2>(hl, dim3(grid.x * 2), block, lds, st, a...);
+            launch_grp_hl<G, U, V, false, false, 2>(hl, false, dim3(grid.x * 2), block, lds, st,
+                                                    a...);
             return;
         }
         if (split == 4) {
-            launch_grp_hl<G, U, V, false, false, 4>(hl, dim3(grid.x * 4), block, lds, st, a...);
+            launch_grp_hl<G, U, V, false, false, 4>(hl, false, dim3(grid.x * 4), block, lds, st,
+                                                    a...);
             return;
         }
     }
-    launch_grp_hl<G, U, V, false, KINK, 1>(hl, grid, block, lds, st, a...);
+    launch_grp_hl<G, U, V, false, KINK, 1>(hl, lean && !KINK, grid, block, lds, st, a...);
 }
 
 // the kink-sum forward is instantiated for the lane groups of HF = 64 heads
@@ -878,7 +899,7 @@ static bool kink_grp_ok(int g, int v) { return (g == 16 && v == 1) || (g == 8 &&
 template <int G, int U, int V, class... A>
 static void launch_edge_kink(int pipe, int hl, dim3 grid, dim3 block, hipStream_t st, A... a) {
     if constexpr ((G == 16 && V == 1) || (G == 8 && V == 2))
-        launch_edge_fused<G, U, V, true>(pipe, 1, hl, grid, block, st, a...);
+        launch_edge_fused<G, U, V, true>(pipe, 1, hl, false, grid, block, st, a...);
 }
 
 extern "C" {
@@ -933,7 +954,8 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     // narrow row-major rows then take two float4s per lane (16 rows per wave at
     // HF = 32: CIFAR batch 11.6 -> 8.6 us; a uniform graph gains nothing)
     const bool local_hint = edges_per_row_hint > 0 && (edges_per_row_hint & GAT_HINT_LOCAL);
-    edges_per_row_hint &= ~GAT_HINT_LOCAL;
+    const bool short_rows = edges_per_row_hint > 0 && (edges_per_row_hint & GAT_HINT_SHORT_ROWS);
+    edges_per_row_hint &= ~kHintFlags;
     int vv = edges_per_row_hint >= 128 ? 2 : 1;
     if (local_hint && !sliced && round_up4(hf) <= 32) vv = 2;
     if (const char* ev = knob("GAT_EDGE_V")) vv = std::atoi(ev) >= 2 ? 2 : 1;
@@ -1021,6 +1043,14 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
             if (split != 2 && split != 4) split = 1;
         }
         if (kink || pipe) split = 1;
+        // the lean instance: every row short (the caller's GAT_HINT_SHORT_ROWS),
+        // no dropout, the plain eval forward.  Opt-in (GAT_EDGE_LEAN=1) until
+        // timed against the full instance on the GPU
+        bool lean = short_rows && drop.thresh == 0u && !kink;
+        {
+            const char* el = knob("GAT_EDGE_LEAN");
+            lean = lean && el != nullptr && std::atoi(el) != 0;
+        }
         if ((long long)blocks * split >= (1LL << 31)) split = 1;
         if (kink && !kink_grp_ok(g, vv)) return GAT_EUNSUPPORTED;
 #define GAT_GRP_KARGS                                                                         \
@@ -1031,7 +1061,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     if (kink)                                                                         \
         launch_edge_kink<G, UU, VV>(pipe, hl, grid, block, st, GAT_GRP_KARGS);         \
     else if (fused)                                                                   \
-        launch_edge_fused<G, UU, VV>(pipe, split, hl, grid, block, st, GAT_GRP_KARGS); \
+        launch_edge_fused<G, UU, VV>(pipe, split, hl, lean, grid, block, st, GAT_GRP_KARGS); \
     else                                                                              \
         hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, GAT_GRP_KARGS)
 #define GAT_GRP_U(G, VV)                                                              \

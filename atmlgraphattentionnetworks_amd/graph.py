@@ -41,6 +41,11 @@ class HubPlan(NamedTuple):
     seg_slot: Optional[torch.Tensor] = None
 
 
+# rows shorter than this are summed without compensation by the edge kernels
+# (gat_edge.hip: the Kahan sums start at 1024 in-edges)
+SHORT_ROW_EDGES = 1024
+
+
 class CSRGraph(NamedTuple):
     rowptr: torch.Tensor  # int32 [N+1]
     col: torch.Tensor  # int32 [E+N], source node ids, ascending within each row
@@ -49,12 +54,20 @@ class CSRGraph(NamedTuple):
     order: Optional[torch.Tensor] = None  # int32 [N], rows by descending in-degree
     hubs: Optional[HubPlan] = None  # split schedule for rows far above the average
     local: bool = False  # sources lie near their targets in node order (locality_hint)
+    max_degree: int = 0  # the longest row's in-edges (0: unknown)
 
     def kernel_hint(self) -> int:
         """The edge kernels' scheduling hint: E'/N, with GAT_HINT_LOCAL OR'd in
-        for a local graph (include/gat_amd.h)."""
+        for a local graph and GAT_HINT_SHORT_ROWS when every row has fewer than
+        1024 in-edges (include/gat_amd.h)."""
         h = self.num_edges // max(self.num_nodes, 1)
-        return h | _lib.GAT_HINT_LOCAL if self.local and h > 0 else h
+        if h <= 0:
+            return h
+        if self.local:
+            h |= _lib.GAT_HINT_LOCAL
+        if 0 < self.max_degree < SHORT_ROW_EDGES:
+            h |= _lib.GAT_HINT_SHORT_ROWS
+        return h
 
 
 def _check_edge_index(edge_index: torch.Tensor, device: torch.device) -> torch.Tensor:
@@ -91,12 +104,20 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int,
     _lib.check(lib.gat_csr_build(ei.data_ptr(), E, num_nodes, rowptr.data_ptr(), col.data_ptr(),
                                  order.data_ptr(), ws.data_ptr(), ws.numel(), flag.data_ptr(),
                                  stream), "gat_csr_build")
-    if int(flag.item()) != 0:
+    # the range flag and the longest row (order[0]: rows by descending degree)
+    # in one device -> host read
+    if num_nodes > 0:
+        top = order[:1].to(torch.int64).clamp_(0, num_nodes - 1)  # in bounds even if bad
+        maxdeg = (rowptr[top + 1] - rowptr[top]).to(torch.int32)
+        bad, max_degree = torch.cat([flag, maxdeg]).tolist()
+    else:
+        bad, max_degree = int(flag.item()), 0
+    if bad != 0:
         # PyG's index_select raises on the same input (GAT.py:53 -> __lift__)
         raise ValueError(f"edge_index contains node ids outside [0, {num_nodes})")
     return CSRGraph(rowptr, col, num_nodes, E + num_nodes, order,
                     hub_plan(rowptr, order, E + num_nodes, col=col),
-                    locality_hint(rowptr, col, num_nodes))
+                    locality_hint(rowptr, col, num_nodes), int(max_degree))
 
 
 def locality_hint(rowptr: torch.Tensor, col: torch.Tensor, num_nodes: int,

@@ -36,6 +36,9 @@ VARIANTS = {
     "pipe_u8_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "8", "GAT_EDGE_V": "2"},
     # the head's lane count read at run time instead of the HL-specialised kernels
     "hl_runtime": {"GAT_EDGE_HL": "0"},
+    # short-row graphs: the lean kernel (no Kahan, no dropout code) that
+    # GAT_HINT_SHORT_ROWS allows (opt-in until timed)
+    "lean": {"GAT_EDGE_LEAN": "1"},
     "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
     "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds", "GAT_EDGE_SCHED": "0"},
     # the CSR-order launch (short rows take the scheduled copy by default)
@@ -72,7 +75,7 @@ def variant(request, monkeypatch):
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
               "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
-              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT"):
+              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_LEAN"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -544,3 +547,25 @@ def test_layer_copy_and_pickle_after_eval_forward(edges):
     del ei
     gc.collect()
     assert csr_ref() is None
+
+
+def test_csr_max_degree_and_short_rows_hint():
+    """build_csr records the longest row (order[0]'s in-degree, self-loop
+    included) and the kernel hint carries GAT_HINT_SHORT_ROWS exactly when
+    every row has fewer than 1024 in-edges."""
+    from atmlgraphattentionnetworks_amd import _lib
+    from atmlgraphattentionnetworks_amd.graph import build_csr
+    d = dev()
+    rng = np.random.default_rng(5)
+    for hub_deg in (0, 1022, 1023, 5000):
+        n, e = 3000, 20000
+        dst = rng.integers(0, n, size=e)
+        if hub_deg:
+            dst = np.concatenate([dst, np.full(hub_deg, 7)])
+        src = rng.integers(0, n, size=dst.size)
+        ei = torch.from_numpy(np.stack([src, dst]).astype(np.int64)).to(d)
+        csr = build_csr(ei, n)
+        deg = np.bincount(dst, minlength=n) + 1  # + the self-loop
+        assert csr.max_degree == int(deg.max())
+        short = bool(csr.kernel_hint() & _lib.GAT_HINT_SHORT_ROWS)
+        assert short == (int(deg.max()) < 1024)
