@@ -271,6 +271,18 @@ constexpr int kHintFlags = GAT_HINT_LOCAL | GAT_HINT_SHORT_ROWS;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
+// Small-Fin fused forward (gat_layer_forward with fin <= 8): the edge kernel
+// gathers the source's x row (fin floats) instead of its Wh row and projects it
+// in registers; no Wh table, no projection launch.
+struct XProjArgs {
+    const float* x;      // [n, fin]
+    const float* w;      // [heads*f, fin]
+    const float* b;      // [heads*f]
+    const float* a_dst;  // [heads*f]
+    const float* c_dst;  // [heads]
+    int fin;
+};
+
 struct EdgeRows {
     const int* eb;     // segment begin (CSR position), indexed by row id or position
     const int* ee;     // segment end

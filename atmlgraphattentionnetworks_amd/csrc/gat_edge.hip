@@ -220,8 +220,14 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 // GAT_HINT_SHORT_ROWS, no dropout): no compensated-sum and no dropout code,
 // whose registers every row otherwise pays for (PPI's short-row instance:
 // 76 -> 60 VGPRs, 6 -> 8 waves per SIMD).
+// XF (> 0): the small-Fin fused forward (fin <= XF): each gathered source's
+// x row is projected in registers (Wh_j = x_j W^T + b for the lane's four
+// columns, the fp32 FMA chain in k order, then + b, as GAT.py:43) and the
+// target's s_dst is formed the same way from x_i; the kernel reads no Wh
+// table.  At CIFAR's Fin = 3 a gathered edge is 12 B of x instead of a 128-B
+// or 256-B Wh row, and the projection launch disappears.
 template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1,
-          int HL = 0, bool LEAN = false>
+          int HL = 0, bool LEAN = false, int XF = 0>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -231,9 +237,10 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const float* __restrict__ bias, float* __restrict__ out, int ld_out,
     float* __restrict__ lse, DropArgs drop_arg, float* __restrict__ y_heads,
     int nslices, int slice_w, long long slice_stride, float* __restrict__ q_heads,
-    float* __restrict__ r_heads, int store_wt) {
+    float* __restrict__ r_heads, int store_wt, XProjArgs xp) {
     const DropArgs drop = resolve_drop(drop_arg);
     static_assert(S == 1 || ((S == 2 || S == 4) && !KINK && !PIPE && G * S <= kWave), "split rows");
+    static_assert(XF == 0 || (V == 1 && FUSED && !KINK && !PIPE && S == 1), "small-Fin form");
     // col values held per lane per chunk.  Groups of >= 4 lanes: every quad of
     // the group holds the chunk's indices (lane c: edges (c & 3) + 4t), so the
     // source ids are broadcast by DPP within the quad instead of LDS permutes
@@ -272,13 +279,60 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         }
         c1 = c_src[h];
     }
+    // XF: the lane's four columns of W and b (zero past fin and past HF)
+    float wl[4][XF > 0 ? XF : 1], bl[4];
+    if constexpr (XF > 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int cc = c_ok ? coff + q : 0;
+            bl[q] = c_ok ? xp.b[cc] : 0.f;
+#pragma unroll
+            for (int k = 0; k < XF; ++k) {
+                const float wv = xp.w[(size_t)cc * xp.fin + min(k, xp.fin - 1)];
+                wl[q][k] = c_ok && k < xp.fin ? wv : 0.f;
+            }
+        }
+    }
+    // x_j W^T + b for the lane's columns; k past fin contributes an exact 0 (the
+    // clamped load's value is replaced, so an infinite x cannot meet a zero W)
+    auto xproj = [&](int j) {
+        f32x4 wh = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (XF > 0) {
+            const float* xr = xp.x + (size_t)j * xp.fin;
+            float xv[XF];
+#pragma unroll
+            for (int k = 0; k < XF; ++k) {
+                const float t = xr[min(k, xp.fin - 1)];
+                xv[k] = k < xp.fin ? t : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float t = 0.f;
+#pragma unroll
+                for (int k = 0; k < XF; ++k) t = __builtin_fmaf(xv[k], wl[q][k], t);
+                wh[q] = t + bl[q];
+            }
+        }
+        return wh;
+    };
     const int si = er.by_pos ? pos : r;  // segment / state index
     const int e0 = er.eb[si], e1 = er.ee[si];
     const bool kahan = !LEAN && e1 - e0 >= 1024;
     const bool dropping = !LEAN && drop.thresh != 0u;  // kernel-uniform: a scalar branch
     // the target's share of every score, in log2 units (LeakyReLU is positively
     // homogeneous: LReLU(z) log2e = LReLU(z log2e)); + c1 when s_src is recomputed
-    const float sd = (s_dst[(size_t)r * H + h] + c1) * kLog2e;
+    float sdv;
+    if constexpr (XF > 0) {
+        // s_dst[i, h] = Wh_i . a2_h + c2_h from the target's own x row
+        const f32x4 whi = xproj(r);
+        const f32x4 a2v = c_ok ? *reinterpret_cast<const f32x4*>(xp.a_dst + coff)
+                               : f32x4{0.f, 0.f, 0.f, 0.f};
+        const float t = whi.x * a2v.x + whi.y * a2v.y + whi.z * a2v.z + whi.w * a2v.w;
+        sdv = group_sum16(t, HL > 0 ? HL : F / 4) + xp.c_dst[h];
+    } else {
+        sdv = s_dst[(size_t)r * H + h];
+    }
+    const float sd = (sdv + c1) * kLog2e;
     float m = -INFINITY, l = 0.f;  // running max in log2 units
     // rows of >= 1024 edges keep Kahan-compensated running sums (lc, cmp) over
     // per-chunk partial sums: a 10k-edge hub row otherwise accumulates more fp32
@@ -324,10 +378,14 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const float* row = Whs + (size_t)j[u] * ld_wh;
+            if constexpr (XF > 0) {
+                v[u][0] = xproj(j[u]);
+            } else {
+                const float* row = Whs + (size_t)j[u] * ld_wh;
 #pragma unroll
-            for (int q = 0; q < V; ++q) v[u][q] = *reinterpret_cast<const f32x4*>(row + 4 * q);
-            if constexpr (!FUSED) s[u] = Ss[(size_t)j[u] * ld_s + h];
+                for (int q = 0; q < V; ++q) v[u][q] = *reinterpret_cast<const f32x4*>(row + 4 * q);
+                if constexpr (!FUSED) s[u] = Ss[(size_t)j[u] * ld_s + h];
+            }
         }
     };
     // scores, online softmax and accumulation of one gathered chunk
@@ -892,6 +950,29 @@ static void launch_edge_fused(int pipe, int split, int hl, bool lean, dim3 grid,
     launch_grp_hl<G, U, V, false, KINK, 1>(hl, lean && !KINK, grid, block, lds, st, a...);
 }
 
+// the small-Fin fused forward (XF): lane groups of HF = 32 or 64 (G = 8, 16),
+// heads of 4 or 8 columns, U = 4 or 8, fin <= 4 or <= 8
+template <int G, int U, int HL, class... A>
+static void launch_xf_fin(int xf, dim3 grid, dim3 block, hipStream_t st, A... a) {
+    if (xf == 4)
+        hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, false, 4>), grid, block,
+                           0, st, a...);
+    else
+        hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, false, 8>), grid, block,
+                           0, st, a...);
+}
+
+template <int G, class... A>
+static void launch_xf(int u, int hl, int xf, dim3 grid, dim3 block, hipStream_t st, A... a) {
+    if (u == 4) {
+        if (hl == 1) launch_xf_fin<G, 4, 1>(xf, grid, block, st, a...);
+        else launch_xf_fin<G, 4, 2>(xf, grid, block, st, a...);
+    } else {
+        if (hl == 1) launch_xf_fin<G, 8, 1>(xf, grid, block, st, a...);
+        else launch_xf_fin<G, 8, 2>(xf, grid, block, st, a...);
+    }
+}
+
 // the kink-sum forward is instantiated for the lane groups of HF = 64 heads
 // (G = 16 at V = 1, G = 8 at V = 2); kink_grp_ok says which launch it serves
 static bool kink_grp_ok(int g, int v) { return (g == 16 && v == 1) || (g == 8 && v == 2); }
@@ -912,7 +993,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
                                float* out, float* lse, float* y_heads, DropArgs drop,
                                int edges_per_row_hint, void* stream, int nslices = 1,
                                long long slice_stride = 0, float* q_heads = nullptr,
-                               float* r_heads = nullptr) {
+                               float* r_heads = nullptr, const XProjArgs* xp = nullptr) {
     if (act < GAT_ACT_LEAKY_RELU || act > GAT_ACT_HEAD_SOFTMAX) return GAT_EINVAL;
     if (heads <= 0 || f <= 0 || row_begin < 0 || row_end < row_begin || nslices <= 0)
         return GAT_EINVAL;
@@ -959,6 +1040,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     int vv = edges_per_row_hint >= 128 ? 2 : 1;
     if (local_hint && !sliced && round_up4(hf) <= 32) vv = 2;
     if (const char* ev = knob("GAT_EDGE_V")) vv = std::atoi(ev) >= 2 ? 2 : 1;
+    if (xp != nullptr) vv = 1;  // the small-Fin form: four columns per lane
 
     while (vv > 1 && f % (4 * vv) != 0) vv >>= 1;
     const int hl = f / (4 * vv);  // lanes per head
@@ -1053,10 +1135,24 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         }
         if ((long long)blocks * split >= (1LL << 31)) split = 1;
         if (kink && !kink_grp_ok(g, vv)) return GAT_EUNSUPPORTED;
+        const XProjArgs xpa = xp != nullptr ? *xp : XProjArgs{nullptr, nullptr, nullptr, nullptr,
+                                                              nullptr, 0};
 #define GAT_GRP_KARGS                                                                         \
     er, col, row_order, row_begin, row_end, wh, ld_wh, s_src, ld_s, a_src, c_src, s_dst,   \
         heads, f, hf, concat, negative_slope, bias, out, ld_out, lse, drop, y_heads, nslices,  \
-        slice_w, slice_stride, q_heads, r_heads, store_wt
+        slice_w, slice_stride, q_heads, r_heads, store_wt, xpa
+        if (xp != nullptr) {
+            // the small-Fin fused forward: no Wh table, one lane group per row
+            if (!(fused && vv == 1 && !kink && !sliced && (g == 8 || g == 16) &&
+                  (hl == 1 || hl == 2) && xp->fin > 0 && xp->fin <= 8 && (u == 4 || u == 8) &&
+                  xp->x != nullptr && xp->w != nullptr && xp->b != nullptr &&
+                  xp->a_dst != nullptr && xp->c_dst != nullptr))
+                return GAT_EUNSUPPORTED;
+            const int xf = xp->fin <= 4 ? 4 : 8;
+            if (g == 8) launch_xf<8>(u, hl, xf, grid, block, st, GAT_GRP_KARGS);
+            else launch_xf<16>(u, hl, xf, grid, block, st, GAT_GRP_KARGS);
+            return status_of(hipGetLastError());
+        }
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
     if (kink)                                                                         \
         launch_edge_kink<G, UU, VV>(pipe, hl, grid, block, st, GAT_GRP_KARGS);         \
@@ -1216,6 +1312,32 @@ int gat_layer_forward(const float* x, int n, int fin, const float* w, const floa
     if (heads <= 0 || f <= 0 || slices <= 0 || n < 0) return GAT_EINVAL;
     const int hf = heads * f, hfp = round_up4(hf);
     int rc;
+    // small Fin (<= 8: CIFAR's 3): the projection fused into the edge kernel,
+    // which gathers x rows instead of Wh rows (k_edge_grp<..., XF>); wh, s_src
+    // and s_dst are then not written.  GAT_EDGE_XPROJ=0 (A/B knob): project, then
+    // aggregate.  Shapes it does not take (GAT_EUNSUPPORTED, nothing launched)
+    // take the two-kernel path below.
+    bool xproj_on = fin > 0 && fin <= 8 && x != nullptr && n > 0;
+    if (const char* v = knob("GAT_EDGE_XPROJ")) xproj_on = xproj_on && std::atoi(v) != 0;
+    if (xproj_on) {
+        if (seg_begin == nullptr || seg_end == nullptr || a_src == nullptr || c_src == nullptr)
+            return GAT_EINVAL;
+        EdgeRows er;
+        er.eb = seg_begin;
+        er.ee = seg_end;
+        er.st_acc = nullptr;
+        er.st_ml = nullptr;
+        er.ld_st = hfp;
+        er.by_pos = 1;
+        er.load = 0;
+        er.store_lt = 0;
+        const XProjArgs xp{x, w, b, a_dst, c_dst, fin};
+        rc = edge_aggregate_impl(er, col, row_order, 0, n, x, hfp, nullptr, 0, a_src, c_src,
+                                 nullptr, heads, f, concat, GAT_ACT_LEAKY_RELU, negative_slope,
+                                 bias, out, nullptr, nullptr, make_drop(0.f, 0ull),
+                                 edges_per_row_hint, stream, 1, 0, nullptr, nullptr, &xp);
+        if (rc != GAT_EUNSUPPORTED) return rc;
+    }
     if (slices > 1)
         rc = gat_project_sliced(x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, slices, wh,
                                 n, nullptr, heads, s_dst, stream);

@@ -295,6 +295,14 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
                 plan.project(lib, x, pp)
         gp.replay()
         proj_ms = _events_ms(gp.replay, 1, stream) / edge_iters
+        fused = fused_small_fin(w.in_channels, plan)
+        if fused:
+            # Fin <= 8: the layer's forward is ONE kernel (gat_layer_forward fuses
+            # the projection into the edge kernel); time exactly that launch
+            for _ in range(3):
+                plan.run(lib, x, pp, bias, out, csr)
+            edge_ms = _events_ms(lambda: plan.run(lib, x, pp, bias, out, csr), edge_iters,
+                                 stream)
     hf = w.heads * w.out_channels
     comp = edge_kernel_compulsory_bytes(n, n, e_prime, w.heads, w.out_channels, w.concat)
     alg = edge_kernel_bytes(n, e_prime, w.heads, w.out_channels, w.concat)
@@ -307,7 +315,9 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
         "value": e_prime / (ms * 1e-3), "unit": "edges/s", "ms_per_step": ms, "launch": launch,
         "csr_build_once_ms": csr_ms, "csr_build_warm_ms": csr_warm_ms,
         "edge_kernel": {
-            "kernel": plan.kernel_name(), "ms": edge_ms,
+            "kernel": ("k_edge_grp<..., XF> with the projection fused (gat_layer_forward, "
+                       "Fin <= 8; x rows gathered, not Wh rows)") if fused else plan.kernel_name(),
+            "ms": edge_ms,
             "edges_per_s": e_prime / es,
             "compulsory_bytes": comp, "compulsory_GBps": comp / es / 1e9,
             "hbm_frac": comp / es / 1e9 / HBM_PEAK_GBS,
@@ -316,13 +326,24 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
             "effective_gather_GBps": alg / es / 1e9,
             "hub_rows_split": 0 if csr.hubs is None else csr.hubs.n_hub,
         },
-        "projection": dict(ms=proj_ms, **projection_roofline(
-            flops, projection_bytes(n, w.in_channels, hf, w.heads), proj_ms, w.in_channels)),
+        "projection": ({"ms": 0.0, "kernel": "fused into the edge kernel (Fin <= 8)",
+                        "two_kernel_projection_ms": proj_ms} if fused else
+                       dict(ms=proj_ms, **projection_roofline(
+                           flops, projection_bytes(n, w.in_channels, hf, w.heads), proj_ms,
+                           w.in_channels))),
         "_inputs": (x, ei, layer),
     }
     _log(f"{name}: {res['value'] / 1e9:.2f} G edges/s, edge {edge_ms * 1e3:.1f} us, "
          f"projection {proj_ms * 1e3:.1f} us")
     return res
+
+
+def fused_small_fin(fin: int, plan) -> bool:
+    """Whether the layer's eval forward runs the fused small-Fin kernel:
+    gat_layer_forward (the cached plan over the scheduled CSR) with Fin <= 8,
+    unless GAT_EDGE_XPROJ=0 (gat_edge.hip)."""
+    return (0 < fin <= 8 and plan.sched is not None and not plan.split
+            and os.environ.get("GAT_EDGE_XPROJ", "1") != "0")
 
 
 def pmc_child(names) -> None:
@@ -347,9 +368,13 @@ def pmc_child(names) -> None:
             bias = layer.bias.detach()
             plan = ForwardPlan(x, csr, w.heads, w.out_channels, w.concat, layer.negative_slope)
             out = torch.empty(x.size(0), w.heads * w.out_channels, device=dev)
+            fused = fused_small_fin(w.in_channels, plan)
             for _ in range(4):
-                plan.project(lib, x, pp)
-                plan.edge(lib, csr, pp, bias, out)
+                if fused:  # one kernel: the layer's own launch
+                    plan.run(lib, x, pp, bias, out, csr)
+                else:
+                    plan.project(lib, x, pp)
+                    plan.edge(lib, csr, pp, bias, out)
             torch.cuda.synchronize()
         # a marker between workloads (the parent splits the dispatch list here)
         torch.zeros(1, device=dev).add_(1)
@@ -720,12 +745,12 @@ def main():
                          "csr_build_once": head["csr_build_once_ms"],
                          "csr_build_warm": head["csr_build_warm_ms"]},
         "projection": {"bound": "mfma", "kernel": head["projection"]["kernel"],
-                       "mfma_dtype": head["projection"]["mfma_dtype"],
-                       "achieved": head["projection"]["mfma_issued_TFLOPs"],
-                       "peak": head["projection"]["mfma_peak_TFLOPs"], "unit": "TFLOP/s",
-                       "frac": head["projection"]["mfma_frac"],
+                       "mfma_dtype": head["projection"].get("mfma_dtype"),
+                       "achieved": head["projection"].get("mfma_issued_TFLOPs"),
+                       "peak": head["projection"].get("mfma_peak_TFLOPs"), "unit": "TFLOP/s",
+                       "frac": head["projection"].get("mfma_frac"),
                        "mfma_busy_frac_pmc": head_sum["projection"].get("mfma_busy_frac_pmc"),
-                       "hbm_frac": head["projection"]["hbm_frac"]},
+                       "hbm_frac": head["projection"].get("hbm_frac")},
         "workloads": workloads,
     }
     if emulated:

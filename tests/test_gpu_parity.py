@@ -39,6 +39,9 @@ VARIANTS = {
     # short-row graphs: the lean kernel (no Kahan, no dropout code) that
     # GAT_HINT_SHORT_ROWS allows (opt-in until timed)
     "lean": {"GAT_EDGE_LEAN": "1"},
+    # Fin <= 8: projection and edge kernel as two launches instead of the fused
+    # small-Fin kernel (the default through gat_layer_forward)
+    "no_xproj": {"GAT_EDGE_XPROJ": "0"},
     "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
     "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds", "GAT_EDGE_SCHED": "0"},
     # the CSR-order launch (short rows take the scheduled copy by default)
@@ -75,7 +78,8 @@ def variant(request, monkeypatch):
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
               "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
-              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_LEAN"):
+              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_LEAN",
+              "GAT_EDGE_XPROJ"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -569,3 +573,37 @@ def test_csr_max_degree_and_short_rows_hint():
         assert csr.max_degree == int(deg.max())
         short = bool(csr.kernel_hint() & _lib.GAT_HINT_SHORT_ROWS)
         assert short == (int(deg.max()) < 1024)
+
+
+@pytest.mark.parametrize("fin", [1, 3, 4, 5, 8])
+@pytest.mark.parametrize("hfc", [(4, 8, True), (8, 8, True), (8, 8, False), (16, 4, True),
+                                 (4, 4, False)],
+                         ids=["H4F8_cat", "H8F8_cat", "H8F8_mean", "H16F4_cat", "H4F4_mean"])
+def test_small_fin_fused_forward(fin, hfc, monkeypatch):
+    """Fin <= 8 (CIFAR's 3): gat_layer_forward fuses the projection into the
+    edge kernel, which gathers x rows and projects them in registers
+    (k_edge_grp<..., XF>).  Against the oracle at the parity bar, and against
+    the two-kernel path (GAT_EDGE_XPROJ=0) with non-finite x in a few rows:
+    the same Inf / NaN pattern."""
+    from atmlgraphattentionnetworks_amd import tuning
+    H, F, concat = hfc
+    x, ei, state = random_case(700, 8000, fin, H, F, concat, seed=31 * fin + H)
+    ref = gat_layer_forward_from_state(state, x, ei, H, concat)
+    outs = {}
+    xb = x.clone()
+    xb[5, 0] = float("inf")
+    xb[77, fin - 1] = float("nan")
+    xb[300, 0] = float("-inf")
+    for xproj in ("1", "0"):
+        monkeypatch.setenv("GAT_EDGE_XPROJ", xproj)
+        tuning.reload()
+        layer = layer_from_state(state, fin, F, H, concat)
+        outs[xproj] = run_layer(layer, x, ei)
+        outs[xproj + "_bad"] = run_layer(layer, xb, ei)
+    torch.testing.assert_close(outs["1"], ref, atol=ATOL, rtol=RTOL)
+    torch.testing.assert_close(outs["1"], outs["0"], atol=ATOL, rtol=RTOL)
+    assert torch.equal(torch.isnan(outs["1_bad"]), torch.isnan(outs["0_bad"]))
+    assert torch.equal(torch.isinf(outs["1_bad"]), torch.isinf(outs["0_bad"]))
+    fin_rows = torch.isfinite(outs["0_bad"]).all(1)
+    torch.testing.assert_close(outs["1_bad"][fin_rows], outs["0_bad"][fin_rows], atol=ATOL,
+                               rtol=RTOL)
