@@ -18,7 +18,7 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 9
+GAT_ABI_VERSION = 10
 GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
 GAT_HINT_SHORT_ROWS = 1 << 29  # every row < 1024 in-edges (include/gat_amd.h)
 GAT_SEG_LOAD = 1

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 9
+#define GAT_ABI_VERSION 10
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -127,7 +127,7 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
  * (block-diagonal batches of small graphs, kNN graphs), so rows processed
  * together share source rows.  Never affects results. */
 #define GAT_HINT_LOCAL (1 << 30)
-/* Scheduling hint bit: no row of the launch has 1024 or more in-edges.  The
+/* Scheduling hint bit (ABI 10): no row of the launch has 1024 or more in-edges.  The
  * edge kernels then skip the compensated (Kahan) summation they keep on such
  * rows, which needs registers every row pays for.  If the promise is broken,
  * long rows are summed plainly (as the reference's own scatter-add does): a
@@ -281,6 +281,11 @@ int gat_edge_merge_ex(const int* hub_rows, const int* seg_ptr, const int* seg_sl
  * target row_order[p]; rows 0 .. n).  Replaces GAT.py:37-67 + GAT.py:54 for a
  * graph whose self-loops are already in the CSR.  Returns the first failing
  * call's status (GAT_EUNSUPPORTED from the projection launches nothing).
+ * ABI 10: with 0 < fin <= 8 the projection is fused into the edge kernel (one
+ * launch that gathers x rows and projects them in registers) wherever that
+ * kernel takes the shape (heads*f of 32 or 64 in heads of 4 or 8 columns,
+ * 4-8 edges per chunk); wh, s_src and s_dst are then scratch the call does
+ * not write.  Results are the two-launch path's up to fp32 rounding.
  */
 int gat_layer_forward(const float* x, int n, int fin, const float* w, const float* b,
                       const float* a_src, const float* c_src, const float* a_dst,
