@@ -265,9 +265,6 @@ __device__ __forceinline__ void store_out1(float* base, size_t idx, float v, int
     }
 }
 
-// the hint's flag bits (include/gat_amd.h); the rest is the edges-per-row count
-constexpr int kHintFlags = GAT_HINT_LOCAL | GAT_HINT_SHORT_ROWS;
-
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 

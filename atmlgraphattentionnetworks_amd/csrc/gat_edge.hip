@@ -216,18 +216,19 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 // HL (> 0): the head's lane count F/4V as a constant (the launcher
 // instantiates it for the HF = 64 lane groups), so the per-edge score sums
 // compile without branches; 0: read from F at run time.
-// LEAN: the eval forward over rows all shorter than 1024 edges (the caller's
-// GAT_HINT_SHORT_ROWS, no dropout): no compensated-sum and no dropout code,
-// whose registers every row otherwise pays for (PPI's short-row instance:
-// 76 -> 60 VGPRs, 6 -> 8 waves per SIMD).
-// XF (> 0): the small-Fin fused forward (fin <= XF): each gathered source's
+// XF (> 0): the small-Fin fused forward (fin == XF <= 4): each gathered source's
 // x row is projected in registers (Wh_j = x_j W^T + b for the lane's four
 // columns, the fp32 FMA chain in k order, then + b, as GAT.py:43) and the
 // target's s_dst is formed the same way from x_i; the kernel reads no Wh
 // table.  At CIFAR's Fin = 3 a gathered edge is 12 B of x instead of a 128-B
 // or 256-B Wh row, and the projection launch disappears.
+template <int N>
+struct XRow {  // one x row of the small-Fin form: N floats, 4-B aligned
+    float v[N];
+};
+
 template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1,
-          int HL = 0, bool LEAN = false, int XF = 0>
+          int HL = 0, int XF = 0>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
         }
         c1 = c_src[h];
     }
-    // XF: the lane's four columns of W and b (zero past fin and past HF)
+    // XF (= fin): the lane's four columns of W and b (zero past HF)
     float wl[4][XF > 0 ? XF : 1], bl[4];
     if constexpr (XF > 0) {
 #pragma unroll
@@ -288,28 +289,23 @@ __global__ __launch_bounds__(256) void k_edge_grp(
             bl[q] = c_ok ? xp.b[cc] : 0.f;
 #pragma unroll
             for (int k = 0; k < XF; ++k) {
-                const float wv = xp.w[(size_t)cc * xp.fin + min(k, xp.fin - 1)];
-                wl[q][k] = c_ok && k < xp.fin ? wv : 0.f;
+                const float wv = xp.w[(size_t)cc * XF + k];
+                wl[q][k] = c_ok ? wv : 0.f;
             }
         }
     }
-    // x_j W^T + b for the lane's columns; k past fin contributes an exact 0 (the
-    // clamped load's value is replaced, so an infinite x cannot meet a zero W)
+    // x_j W^T + b for the lane's columns: the row's XF floats in ONE load
+    // (global_load_dwordx<XF>; per-element loads made the kernel load-issue
+    // bound), then the fp32 FMA chain in k order
     auto xproj = [&](int j) {
         f32x4 wh = f32x4{0.f, 0.f, 0.f, 0.f};
         if constexpr (XF > 0) {
-            const float* xr = xp.x + (size_t)j * xp.fin;
-            float xv[XF];
-#pragma unroll
-            for (int k = 0; k < XF; ++k) {
-                const float t = xr[min(k, xp.fin - 1)];
-                xv[k] = k < xp.fin ? t : 0.f;
-            }
+            const XRow<XF> xr = *reinterpret_cast<const XRow<XF>*>(xp.x + (size_t)j * XF);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float t = 0.f;
 #pragma unroll
-                for (int k = 0; k < XF; ++k) t = __builtin_fmaf(xv[k], wl[q][k], t);
+                for (int k = 0; k < XF; ++k) t = __builtin_fmaf(xr.v[k], wl[q][k], t);
                 wh[q] = t + bl[q];
             }
         }
@@ -317,8 +313,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     };
     const int si = er.by_pos ? pos : r;  // segment / state index
     const int e0 = er.eb[si], e1 = er.ee[si];
-    const bool kahan = !LEAN && e1 - e0 >= 1024;
-    const bool dropping = !LEAN && drop.thresh != 0u;  // kernel-uniform: a scalar branch
+    const bool kahan = e1 - e0 >= 1024;
+    const bool dropping = drop.thresh != 0u;  // kernel-uniform: a scalar branch
     // the target's share of every score, in log2 units (LeakyReLU is positively
     // homogeneous: LReLU(z) log2e = LReLU(z log2e)); + c1 when s_src is recomputed
     float sdv;
@@ -883,25 +879,10 @@ __global__ __launch_bounds__(64) void k_edge_merge(
 // and hl is 1 or 2 (heads of 4 or 8 columns); the run-time form otherwise.
 // GAT_EDGE_HL=0 (A/B knob) forces the run-time form.
 template <int G, int U, int V, bool PIPE, bool KINK, int S, class... A>
-static void launch_grp_hl(int hl, bool lean, dim3 grid, dim3 block, size_t lds, hipStream_t st,
-                          A... a) {
+static void launch_grp_hl(int hl, dim3 grid, dim3 block, size_t lds, hipStream_t st, A... a) {
     if constexpr (G == 4 || G == 8 || G == 16) {
         const char* v = knob("GAT_EDGE_HL");
         const bool on = v == nullptr || std::atoi(v) != 0;
-        // the lean eval instance (LEAN): the short-row schedules (V = 1, U = 4
-        // or 8, one lane group per row) of HF = 64's heads
-        if constexpr (V == 1 && (U == 4 || U == 8) && !PIPE && !KINK && S == 1) {
-            if (on && lean && hl == 1) {
-                hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 1, 1, true>), grid,
-                                   block, lds, st, a...);
-                return;
-            }
-            if (on && lean && hl == 2) {
-                hipLaunchKernelGGL((k_edge_grp<G, U, V, true, false, false, 1, 2, true>), grid,
-                                   block, lds, st, a...);
-                return;
-            }
-        }
         if (on && hl == 1) {
             hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1>), grid, block, lds, st, a...);
             return;
@@ -915,8 +896,8 @@ static void launch_grp_hl(int hl, bool lean, dim3 grid, dim3 block, size_t lds, 
 }
 
 template <int G, int U, int V, bool KINK = false, class... A>
-static void launch_edge_fused(int pipe, int split, int hl, bool lean, dim3 grid, dim3 block,
-                              hipStream_t st, A... a) {
+static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block, hipStream_t st,
+                              A... a) {
     // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
     // kernel — caps the blocks resident per CU (160 KB / bytes)
     size_t lds = 0;
@@ -928,7 +909,7 @@ static void launch_edge_fused(int pipe, int split, int hl, bool lean, dim3 grid,
     // 54.0 -> 54.9 us, CIFAR equal; profiles/r05/edge_ab_pipe_short_*.json)
     if constexpr (V == 2 && (U == 16 || U == 8)) {
         if (pipe) {
-            launch_grp_hl<G, U, V, true, KINK, 1>(hl, false, grid, block, lds, st, a...);
+            launch_grp_hl<G, U, V, true, KINK, 1>(hl, grid, block, lds, st, a...);
             return;
         }
     }
@@ -937,29 +918,31 @@ static void launch_edge_fused(int pipe, int split, int hl, bool lean, dim3 grid,
     // row-major)
     if constexpr (!KINK && V == 1 && U <= 8 && (G == 8 || G == 16)) {
         if (split == 2) {
-            launch_grp_hl<G, U, V, false, false, 2>(hl, false, dim3(grid.x * 2), block, lds, st,
-                                                    a...);
+            launch_grp_hl<G, U, V, false, false, 2>(hl, dim3(grid.x * 2), block, lds, st, a...);
             return;
         }
         if (split == 4) {
-            launch_grp_hl<G, U, V, false, false, 4>(hl, false, dim3(grid.x * 4), block, lds, st,
-                                                    a...);
+            launch_grp_hl<G, U, V, false, false, 4>(hl, dim3(grid.x * 4), block, lds, st, a...);
             return;
         }
     }
-    launch_grp_hl<G, U, V, false, KINK, 1>(hl, lean && !KINK, grid, block, lds, st, a...);
+    launch_grp_hl<G, U, V, false, KINK, 1>(hl, grid, block, lds, st, a...);
 }
 
 // the small-Fin fused forward (XF): lane groups of HF = 32 or 64 (G = 8, 16),
-// heads of 4 or 8 columns, U = 4 or 8, fin <= 4 or <= 8
+// heads of 4 or 8 columns, U = 4 or 8, fin 1-4
 template <int G, int U, int HL, class... A>
 static void launch_xf_fin(int xf, dim3 grid, dim3 block, hipStream_t st, A... a) {
-    if (xf == 4)
-        hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, false, 4>), grid, block,
-                           0, st, a...);
-    else
-        hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, false, 8>), grid, block,
-                           0, st, a...);
+#define GAT_XF(N)                                                                               \
+    hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, N>), grid, block,        \
+                       0, st, a...)
+    switch (xf) {
+        case 1: GAT_XF(1); break;
+        case 2: GAT_XF(2); break;
+        case 3: GAT_XF(3); break;
+        default: GAT_XF(4); break;
+    }
+#undef GAT_XF
 }
 
 template <int G, class... A>
@@ -980,7 +963,7 @@ static bool kink_grp_ok(int g, int v) { return (g == 16 && v == 1) || (g == 8 &&
 template <int G, int U, int V, class... A>
 static void launch_edge_kink(int pipe, int hl, dim3 grid, dim3 block, hipStream_t st, A... a) {
     if constexpr ((G == 16 && V == 1) || (G == 8 && V == 2))
-        launch_edge_fused<G, U, V, true>(pipe, 1, hl, false, grid, block, st, a...);
+        launch_edge_fused<G, U, V, true>(pipe, 1, hl, grid, block, st, a...);
 }
 
 extern "C" {
@@ -1035,8 +1018,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     // narrow row-major rows then take two float4s per lane (16 rows per wave at
     // HF = 32: CIFAR batch 11.6 -> 8.6 us; a uniform graph gains nothing)
     const bool local_hint = edges_per_row_hint > 0 && (edges_per_row_hint & GAT_HINT_LOCAL);
-    const bool short_rows = edges_per_row_hint > 0 && (edges_per_row_hint & GAT_HINT_SHORT_ROWS);
-    edges_per_row_hint &= ~kHintFlags;
+    edges_per_row_hint &= ~GAT_HINT_LOCAL;
     int vv = edges_per_row_hint >= 128 ? 2 : 1;
     if (local_hint && !sliced && round_up4(hf) <= 32) vv = 2;
     if (const char* ev = knob("GAT_EDGE_V")) vv = std::atoi(ev) >= 2 ? 2 : 1;
@@ -1125,14 +1107,6 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
             if (split != 2 && split != 4) split = 1;
         }
         if (kink || pipe) split = 1;
-        // the lean instance: every row short (the caller's GAT_HINT_SHORT_ROWS),
-        // no dropout, the plain eval forward.  Opt-in (GAT_EDGE_LEAN=1) until
-        // timed against the full instance on the GPU
-        bool lean = short_rows && drop.thresh == 0u && !kink;
-        {
-            const char* el = knob("GAT_EDGE_LEAN");
-            lean = lean && el != nullptr && std::atoi(el) != 0;
-        }
         if ((long long)blocks * split >= (1LL << 31)) split = 1;
         if (kink && !kink_grp_ok(g, vv)) return GAT_EUNSUPPORTED;
         const XProjArgs xpa = xp != nullptr ? *xp : XProjArgs{nullptr, nullptr, nullptr, nullptr,
@@ -1144,11 +1118,11 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         if (xp != nullptr) {
             // the small-Fin fused forward: no Wh table, one lane group per row
             if (!(fused && vv == 1 && !kink && !sliced && (g == 8 || g == 16) &&
-                  (hl == 1 || hl == 2) && xp->fin > 0 && xp->fin <= 8 && (u == 4 || u == 8) &&
+                  (hl == 1 || hl == 2) && xp->fin > 0 && xp->fin <= 4 && (u == 4 || u == 8) &&
                   xp->x != nullptr && xp->w != nullptr && xp->b != nullptr &&
                   xp->a_dst != nullptr && xp->c_dst != nullptr))
                 return GAT_EUNSUPPORTED;
-            const int xf = xp->fin <= 4 ? 4 : 8;
+            const int xf = xp->fin;
             if (g == 8) launch_xf<8>(u, hl, xf, grid, block, st, GAT_GRP_KARGS);
             else launch_xf<16>(u, hl, xf, grid, block, st, GAT_GRP_KARGS);
             return status_of(hipGetLastError());
@@ -1157,7 +1131,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     if (kink)                                                                         \
         launch_edge_kink<G, UU, VV>(pipe, hl, grid, block, st, GAT_GRP_KARGS);         \
     else if (fused)                                                                   \
-        launch_edge_fused<G, UU, VV>(pipe, split, hl, lean, grid, block, st, GAT_GRP_KARGS); \
+        launch_edge_fused<G, UU, VV>(pipe, split, hl, grid, block, st, GAT_GRP_KARGS); \
     else                                                                              \
         hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, GAT_GRP_KARGS)
 #define GAT_GRP_U(G, VV)                                                              \
@@ -1312,12 +1286,12 @@ int gat_layer_forward(const float* x, int n, int fin, const float* w, const floa
     if (heads <= 0 || f <= 0 || slices <= 0 || n < 0) return GAT_EINVAL;
     const int hf = heads * f, hfp = round_up4(hf);
     int rc;
-    // small Fin (<= 8: CIFAR's 3): the projection fused into the edge kernel,
+    // small Fin (<= 4: CIFAR's 3): the projection fused into the edge kernel,
     // which gathers x rows instead of Wh rows (k_edge_grp<..., XF>); wh, s_src
     // and s_dst are then not written.  GAT_EDGE_XPROJ=0 (A/B knob): project, then
     // aggregate.  Shapes it does not take (GAT_EUNSUPPORTED, nothing launched)
     // take the two-kernel path below.
-    bool xproj_on = fin > 0 && fin <= 8 && x != nullptr && n > 0;
+    bool xproj_on = fin > 0 && fin <= 4 && x != nullptr && n > 0;
     if (const char* v = knob("GAT_EDGE_XPROJ")) xproj_on = xproj_on && std::atoi(v) != 0;
     if (xproj_on) {
         if (seg_begin == nullptr || seg_end == nullptr || a_src == nullptr || c_src == nullptr)

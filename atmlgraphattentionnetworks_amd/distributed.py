@@ -122,15 +122,7 @@ class LocalCSR:
     num_edges: int
     order: Optional[torch.Tensor] = None  # int32 [n_local], rows by descending in-degree
     seg: Optional[torch.Tensor] = None  # int32 [chunks + 1, n_local]: pass c = [seg[c], seg[c+1])
-    max_degree: int = 0  # the longest local row's in-edges (0: unknown)
 
-    def kernel_hint(self) -> int:
-        """E'/rows of the local CSR, + GAT_HINT_SHORT_ROWS when every local row
-        has fewer than 1024 in-edges (include/gat_amd.h)."""
-        h = self.num_edges // max(self.num_nodes, 1)
-        if h > 0 and 0 < self.max_degree < 1024:
-            h |= _lib.GAT_HINT_SHORT_ROWS
-        return h
 
 
 def _score(layer):
@@ -227,7 +219,7 @@ class HipOps:
         if n == 0:
             return out
         stream = torch._C._cuda_getCurrentRawStream(table.device.index)
-        hint = local.kernel_hint() if hasattr(local, "kernel_hint") else local.num_edges // max(n, 1)
+        hint = local.num_edges // max(n, 1)
         order = 0 if local.order is None else local.order.data_ptr()
         if layout.kind == "packed":
             if flags:
@@ -427,9 +419,8 @@ class ShardedGAT:
         else:
             seg[1] = lrp[1:].to(torch.int32)
         lrp32 = lrp.to(torch.int32).contiguous()
-        max_degree = int(deg.max()) if self.n_local > 0 else 0
         return LocalCSR(lrp32, trow.to(torch.int32).contiguous(), self.n_local, e1 - e0,
-                        degree_order(lrp32), seg.contiguous(), max_degree)
+                        degree_order(lrp32), seg.contiguous())
 
     # -- the pieces of a step ------------------------------------------------
     def local_x(self, x_full):

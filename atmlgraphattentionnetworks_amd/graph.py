@@ -41,11 +41,6 @@ class HubPlan(NamedTuple):
     seg_slot: Optional[torch.Tensor] = None
 
 
-# rows shorter than this are summed without compensation by the edge kernels
-# (gat_edge.hip: the Kahan sums start at 1024 in-edges)
-SHORT_ROW_EDGES = 1024
-
-
 class CSRGraph(NamedTuple):
     rowptr: torch.Tensor  # int32 [N+1]
     col: torch.Tensor  # int32 [E+N], source node ids, ascending within each row
@@ -58,16 +53,9 @@ class CSRGraph(NamedTuple):
 
     def kernel_hint(self) -> int:
         """The edge kernels' scheduling hint: E'/N, with GAT_HINT_LOCAL OR'd in
-        for a local graph and GAT_HINT_SHORT_ROWS when every row has fewer than
-        1024 in-edges (include/gat_amd.h)."""
+        for a local graph (include/gat_amd.h)."""
         h = self.num_edges // max(self.num_nodes, 1)
-        if h <= 0:
-            return h
-        if self.local:
-            h |= _lib.GAT_HINT_LOCAL
-        if 0 < self.max_degree < SHORT_ROW_EDGES:
-            h |= _lib.GAT_HINT_SHORT_ROWS
-        return h
+        return h | _lib.GAT_HINT_LOCAL if self.local and h > 0 else h
 
 
 def _check_edge_index(edge_index: torch.Tensor, device: torch.device) -> torch.Tensor:

@@ -297,7 +297,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
         proj_ms = _events_ms(gp.replay, 1, stream) / edge_iters
         fused = fused_small_fin(w.in_channels, plan)
         if fused:
-            # Fin <= 8: the layer's forward is ONE kernel (gat_layer_forward fuses
+            # Fin <= 4: the layer's forward is ONE kernel (gat_layer_forward fuses
             # the projection into the edge kernel); time exactly that launch
             for _ in range(3):
                 plan.run(lib, x, pp, bias, out, csr)
@@ -316,7 +316,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
         "csr_build_once_ms": csr_ms, "csr_build_warm_ms": csr_warm_ms,
         "edge_kernel": {
             "kernel": ("k_edge_grp<..., XF> with the projection fused (gat_layer_forward, "
-                       "Fin <= 8; x rows gathered, not Wh rows)") if fused else plan.kernel_name(),
+                       "Fin <= 4; x rows gathered, not Wh rows)") if fused else plan.kernel_name(),
             "ms": edge_ms,
             "edges_per_s": e_prime / es,
             "compulsory_bytes": comp, "compulsory_GBps": comp / es / 1e9,
@@ -326,7 +326,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
             "effective_gather_GBps": alg / es / 1e9,
             "hub_rows_split": 0 if csr.hubs is None else csr.hubs.n_hub,
         },
-        "projection": ({"ms": 0.0, "kernel": "fused into the edge kernel (Fin <= 8)",
+        "projection": ({"ms": 0.0, "kernel": "fused into the edge kernel (Fin <= 4)",
                         "two_kernel_projection_ms": proj_ms} if fused else
                        dict(ms=proj_ms, **projection_roofline(
                            flops, projection_bytes(n, w.in_channels, hf, w.heads), proj_ms,
@@ -340,9 +340,9 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
 
 def fused_small_fin(fin: int, plan) -> bool:
     """Whether the layer's eval forward runs the fused small-Fin kernel:
-    gat_layer_forward (the cached plan over the scheduled CSR) with Fin <= 8,
+    gat_layer_forward (the cached plan over the scheduled CSR) with Fin <= 4,
     unless GAT_EDGE_XPROJ=0 (gat_edge.hip)."""
-    return (0 < fin <= 8 and plan.sched is not None and not plan.split
+    return (0 < fin <= 4 and plan.sched is not None and not plan.split
             and os.environ.get("GAT_EDGE_XPROJ", "1") != "0")
 
 

@@ -117,9 +117,8 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
  *   lse          optional [rows, heads] = max + log(sum exp) per (row, head)
  *                (natural log; for the backward pass); may be NULL
  *   edges_per_row_hint  average in-degree (E'/rows) or 0 if unknown: picks the
- *                edge-chunk length, never affects results; GAT_HINT_LOCAL and
- *                GAT_HINT_SHORT_ROWS may be OR'd in (every entry point taking a
- *                hint accepts them)
+ *                edge-chunk length, never affects results; GAT_HINT_LOCAL may be
+ *                OR'd in (every entry point taking a hint accepts it)
  * GAT_EUNSUPPORTED if s_src is NULL and the shape needs it (f % 4 != 0, or
  * f/4 not a power of two, or negative_slope outside [0, 1]).
  */
@@ -127,12 +126,6 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
  * (block-diagonal batches of small graphs, kNN graphs), so rows processed
  * together share source rows.  Never affects results. */
 #define GAT_HINT_LOCAL (1 << 30)
-/* Scheduling hint bit (ABI 10): no row of the launch has 1024 or more in-edges.  The
- * edge kernels then skip the compensated (Kahan) summation they keep on such
- * rows, which needs registers every row pays for.  If the promise is broken,
- * long rows are summed plainly (as the reference's own scatter-add does): a
- * rounding difference, never a wrong result. */
-#define GAT_HINT_SHORT_ROWS (1 << 29)
 
 int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, int row_begin,
                        int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
@@ -281,7 +274,7 @@ int gat_edge_merge_ex(const int* hub_rows, const int* seg_ptr, const int* seg_sl
  * target row_order[p]; rows 0 .. n).  Replaces GAT.py:37-67 + GAT.py:54 for a
  * graph whose self-loops are already in the CSR.  Returns the first failing
  * call's status (GAT_EUNSUPPORTED from the projection launches nothing).
- * ABI 10: with 0 < fin <= 8 the projection is fused into the edge kernel (one
+ * ABI 10: with 0 < fin <= 4 the projection is fused into the edge kernel (one
  * launch that gathers x rows and projects them in registers) wherever that
  * kernel takes the shape (heads*f of 32 or 64 in heads of 4 or 8 columns,
  * 4-8 edges per chunk); wh, s_src and s_dst are then scratch the call does

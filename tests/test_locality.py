@@ -53,15 +53,3 @@ def test_small_graph_never_local_and_hint_bit():
     assert g.kernel_hint() & ~_lib.GAT_HINT_LOCAL == col.numel() // 100
     assert CSRGraph(rowptr, col, 100, int(col.numel())).kernel_hint() == col.numel() // 100
 
-
-def test_short_rows_hint_bit():
-    """GAT_HINT_SHORT_ROWS rides on the hint when the CSR's longest row has
-    fewer than 1024 in-edges (unknown max degree: no bit)."""
-    rowptr, col = _csr(100, np.arange(99), np.arange(1, 100))
-    base = col.numel() // 100
-    assert CSRGraph(rowptr, col, 100, int(col.numel()), max_degree=2).kernel_hint() == \
-        base | _lib.GAT_HINT_SHORT_ROWS
-    assert CSRGraph(rowptr, col, 100, int(col.numel()), max_degree=1024).kernel_hint() == base
-    assert CSRGraph(rowptr, col, 100, int(col.numel())).kernel_hint() == base
-    g = CSRGraph(rowptr, col, 100, int(col.numel()), None, None, True, 5)
-    assert g.kernel_hint() == base | _lib.GAT_HINT_LOCAL | _lib.GAT_HINT_SHORT_ROWS
