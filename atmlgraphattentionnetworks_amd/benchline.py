@@ -94,7 +94,9 @@ def _workload(w: Dict, cpu: Optional[Dict]) -> Dict:
          "project_ms": _get(w, "projection", "ms"), "hbm_frac": r.get("frac"),
          "fabric_x": fab.get("x_compulsory"), "l2_hit": fab.get("l2_hit_rate"),
          "l2_gather_frac": _get(r, "l2", "frac_of_gather_ceiling"),
-         "project_kernel": _get(w, "projection", "kernel")}
+         "project_kernel": _get(w, "projection", "kernel"),
+         "in_step": {k: v for k, v in (w.get("phases_in_step_ms") or {}).items() if k != "what"}
+                    or None}
     if cpu:
         d["cpu_value"] = cpu.get("value")
     tr = w.get("training")

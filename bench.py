@@ -295,6 +295,31 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
                 plan.project(lib, x, pp)
         gp.replay()
         proj_ms = _events_ms(gp.replay, 1, stream) / edge_iters
+        # the two phases IN the step sequence: the layer's ping-pong workspaces
+        # alternating, events between the launches (the isolated timings above
+        # run each phase back to back on its own, so their sum need not equal
+        # the step)
+        seq = ForwardPlan(x, csr, w.heads, w.out_channels, w.concat, layer.negative_slope,
+                          pingpong=True)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(edge_iters)]
+        for i in range(edge_iters + 3):
+            seq.cur ^= 1
+            seq.p_wh, seq.p_ss, seq.p_sd = seq.bufs[seq.cur]
+            e = evs[i - 3] if i >= 3 else None
+            if e:
+                e[0].record(stream)
+            seq.project(lib, x, pp)
+            if e:
+                e[1].record(stream)
+            seq.edge(lib, csr, pp, bias, out)
+            if e:
+                e[2].record(stream)
+        torch.cuda.synchronize()
+        in_step = {"project": statistics.median(a.elapsed_time(b) for a, b, _ in evs),
+                   "edge": statistics.median(b.elapsed_time(c) for _, b, c in evs),
+                   "what": "median per step of events between the two launches in the layer's "
+                           "own sequence (ping-pong workspaces)"}
+        del seq
         fused = fused_small_fin(w.in_channels, plan)
         if fused:
             # Fin <= 4: the layer's forward is ONE kernel (gat_layer_forward fuses
@@ -314,6 +339,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
         "F": w.out_channels, "concat": w.concat,
         "value": e_prime / (ms * 1e-3), "unit": "edges/s", "ms_per_step": ms, "launch": launch,
         "csr_build_once_ms": csr_ms, "csr_build_warm_ms": csr_warm_ms,
+        "phases_in_step_ms": None if fused else in_step,
         "edge_kernel": {
             "kernel": ("k_edge_grp<..., XF> with the projection fused (gat_layer_forward, "
                        "Fin <= 4; x rows gathered, not Wh rows)") if fused else plan.kernel_name(),
@@ -743,7 +769,9 @@ def main():
         "roofline": head_sum["roofline"],
         "breakdown_ms": {"project": head["projection"]["ms"], "edge": head["edge_kernel"]["ms"],
                          "csr_build_once": head["csr_build_once_ms"],
-                         "csr_build_warm": head["csr_build_warm_ms"]},
+                         "csr_build_warm": head["csr_build_warm_ms"],
+                         "in_step": {k: v for k, v in (head.get("phases_in_step_ms") or {}).items()
+                                     if k != "what"}},
         "projection": {"bound": "mfma", "kernel": head["projection"]["kernel"],
                        "mfma_dtype": head["projection"].get("mfma_dtype"),
                        "achieved": head["projection"].get("mfma_issued_TFLOPs"),
