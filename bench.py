@@ -52,22 +52,25 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 matrix peak (v_mfma_f32_16x16x32_bf
 SPLIT_PRODUCTS = 6  # bf16 MFMA products per fp32 product in the split-bf16 projections
 
 
-def projection_kernel(fin: int) -> dict:
-    """The projection kernel the library picks for this Fin (gat_project.hip
-    project_impl, default knobs) and the matrix dtype it issues."""
+def projection_kernel(fin: int, f: int = 8) -> dict:
+    """The projection kernel the library picks for this Fin and head width F
+    (gat_project.hip project_impl, default knobs) and the matrix dtype it issues."""
     if fin <= 64:
         return {"kernel": "k_project_wk", "mfma": "fp32 (v_mfma_f32_16x16x4_f32)",
                 "split": False}
-    name = "k_project_wres" if fin <= 128 else "k_project_x3"
+    if fin <= 128:
+        name = "k_project_wres_d" if f in (4, 8, 16) else "k_project_wres"
+    else:
+        name = "k_project_x3"
     return {"kernel": name, "mfma": "bf16, operands split exactly into 3 bf16 terms, "
             "6 v_mfma_f32_16x16x32_bf16 per fp32 product", "split": True}
 
 
-def projection_roofline(flops: float, nbytes: float, ms: float, fin: int) -> dict:
+def projection_roofline(flops: float, nbytes: float, ms: float, fin: int, f: int = 8) -> dict:
     """fp32-equivalent TFLOP/s, the fraction of the matrix peak of the dtype the
     kernel issues, and the HBM fraction; ``bound`` = the larger of the two time
     bounds."""
-    k = projection_kernel(fin)
+    k = projection_kernel(fin, f)
     sec = ms * 1e-3
     if k["split"]:
         mfma_flops, peak = SPLIT_PRODUCTS * flops, MFMA_BF16_PEAK_TFLOPS
@@ -356,7 +359,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
                         "two_kernel_projection_ms": proj_ms} if fused else
                        dict(ms=proj_ms, **projection_roofline(
                            flops, projection_bytes(n, w.in_channels, hf, w.heads), proj_ms,
-                           w.in_channels))),
+                           w.in_channels, w.out_channels))),
         "_inputs": (x, ei, layer),
     }
     _log(f"{name}: {res['value'] / 1e9:.2f} G edges/s, edge {edge_ms * 1e3:.1f} us, "
