@@ -869,6 +869,93 @@ __global__ __launch_bounds__(64) void k_edge_merge(
 #undef SLOT
 }
 
+// The same merge with a hub's segments spread over a 256-thread workgroup
+// (the default since round 5).  k_edge_merge walks all of a hub's segments in
+// one lane per head / column, three dependent loops of one load each: at
+// power-law Reddit (13k hubs, up to 116 segments) its launch took 120 us, set
+// by the longest hubs' load chains.  Here thread t takes segments
+// s0 + g, s0 + g + ng, ... (g = t / H or t / HF), and the per-group partial
+// maxima / sums are combined in LDS in group order: deterministic, the same
+// segmented softmax regrouped as k_edge_merge (sums in another order).
+__global__ __launch_bounds__(256) void k_edge_merge_wg(
+    const int* __restrict__ hub_rows, const int* __restrict__ vptr,
+    const int* __restrict__ vslot, int n_hub,
+    const float* __restrict__ st_acc, int ld_st, const float* __restrict__ st_ml, int H, int F,
+    int HF, int concat, const float* __restrict__ bias, float* __restrict__ out, int ld_out,
+    float* __restrict__ lse, float* __restrict__ y_heads) {
+    __shared__ float red[256];
+    __shared__ float Ms[GAT_MAX_HEADS], Ls[GAT_MAX_HEADS], ys[GAT_MAX_HF];
+    const int k = blockIdx.x;
+    if (k >= n_hub) return;
+    const int t = threadIdx.x;
+    const int r = hub_rows[k], s0 = vptr[k], s1 = vptr[k + 1];
+#define SLOT(sg) (vslot != nullptr ? vslot[sg] : (sg))
+    // per-head max and sum: head h = t % H, segment group g = t / H of ng
+    const int ng = 256 / H, h = t % H, g = t / H;
+    const bool hact = g < ng;
+    float m = -INFINITY;
+    if (hact)
+        for (int sg = s0 + g; sg < s1; sg += ng)
+            m = fmaxf(m, st_ml[(size_t)SLOT(sg) * 2 * H + h]);
+    red[t] = m;
+    __syncthreads();
+    if (t < H) {
+        float M = -INFINITY;
+        for (int q = 0; q < ng; ++q) M = fmaxf(M, red[q * H + t]);
+        Ms[t] = M;
+    }
+    __syncthreads();
+    float l = 0.f;
+    if (hact) {
+        const float M = Ms[h];
+        for (int sg = s0 + g; sg < s1; sg += ng) {
+            const size_t o = (size_t)SLOT(sg) * 2 * H;
+            const float ms = st_ml[o + h];
+            if (ms != -INFINITY) l += st_ml[o + H + h] * __builtin_amdgcn_exp2f(ms - M);
+        }
+    }
+    red[t] = l;
+    __syncthreads();
+    if (t < H) {
+        float L = 0.f;
+        for (int q = 0; q < ng; ++q) L += red[q * H + t];
+        Ls[t] = L;
+        if (lse != nullptr) lse[(size_t)r * H + t] = (Ms[t] + log2f(L)) * kLn2;
+    }
+    __syncthreads();
+    // columns: column c = t % HF, segment group gc = t / HF of ngc
+    const int ngc = 256 / HF, c = t % HF, gc = t / HF;
+    float a = 0.f;
+    if (gc < ngc) {
+        const int hh = c / F;
+        const float M = Ms[hh];
+        for (int sg = s0 + gc; sg < s1; sg += ngc) {
+            const int sl = SLOT(sg);
+            const float ms = st_ml[(size_t)sl * 2 * H + hh];
+            if (ms != -INFINITY) a += st_acc[(size_t)sl * ld_st + c] * __builtin_amdgcn_exp2f(ms - M);
+        }
+    }
+    red[t] = a;
+    __syncthreads();
+    if (t < HF) {
+        float A = 0.f;
+        for (int q = 0; q < ngc; ++q) A += red[q * HF + t];
+        const float y = A / (Ls[t / F] + 1e-16f);
+        if (y_heads != nullptr) y_heads[(size_t)r * HF + t] = y;
+        if (concat) out[(size_t)r * ld_out + t] = y + bias[t];
+        else ys[t] = y;
+    }
+    if (!concat) {
+        __syncthreads();
+        if (t < F) {
+            float sum = 0.f;
+            for (int q = 0; q < H; ++q) sum += ys[q * F + t];
+            out[(size_t)r * ld_out + t] = sum / (float)H + bias[t];
+        }
+    }
+#undef SLOT
+}
+
 }  // namespace
 
 // Fused lane-group edge kernel, optionally with the gathers pipelined one
@@ -1383,9 +1470,16 @@ int gat_edge_merge_ex(const int* hub_rows, const int* seg_ptr, const int* seg_sl
     if (hub_rows == nullptr || seg_ptr == nullptr || st_acc == nullptr || st_ml == nullptr ||
         bias == nullptr || out == nullptr)
         return GAT_EINVAL;
-    hipLaunchKernelGGL(k_edge_merge, dim3(n_hub), dim3(kWave), 0, (hipStream_t)stream, hub_rows,
-                       seg_ptr, seg_slot, n_hub, st_acc, round_up4(hf), st_ml, heads, f, hf, concat, bias,
-                       out, concat ? hf : f, lse, y_heads);
+    // GAT_EDGE_MERGE=0 (A/B knob): the one-wave-per-hub merge
+    const char* mk = knob("GAT_EDGE_MERGE");
+    if (mk != nullptr && std::atoi(mk) == 0)
+        hipLaunchKernelGGL(k_edge_merge, dim3(n_hub), dim3(kWave), 0, (hipStream_t)stream,
+                           hub_rows, seg_ptr, seg_slot, n_hub, st_acc, round_up4(hf), st_ml, heads,
+                           f, hf, concat, bias, out, concat ? hf : f, lse, y_heads);
+    else
+        hipLaunchKernelGGL(k_edge_merge_wg, dim3(n_hub), dim3(256), 0, (hipStream_t)stream,
+                           hub_rows, seg_ptr, seg_slot, n_hub, st_acc, round_up4(hf), st_ml, heads,
+                           f, hf, concat, bias, out, concat ? hf : f, lse, y_heads);
     return status_of(hipGetLastError());
 }
 

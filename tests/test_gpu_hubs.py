@@ -65,14 +65,18 @@ def _hub_case(n, e_uniform, hubs, fin, H, F, concat, seed):
 @pytest.mark.parametrize("H,F,concat", [(8, 8, True), (8, 8, False), (4, 8, True),
                                         (2, 16, True), (16, 4, False)])
 @pytest.mark.parametrize("slices", ["1", None])
-def test_split_hubs_match_oracle(H, F, concat, slices, monkeypatch):
+@pytest.mark.parametrize("merge", [None, "0"])
+def test_split_hubs_match_oracle(H, F, concat, slices, merge, monkeypatch):
     """GAT_HUB_SEG=64 splits every row above 128 in-edges (here: 5 hubs of
     300-5000 edges, and the long uniform rows are whole); planes (default
-    layout at >= 16 edges/row, concat) and row-major tables."""
+    layout at >= 16 edges/row, concat) and row-major tables; the workgroup
+    merge (default) and the one-wave merge (GAT_EDGE_MERGE=0)."""
     from atmlgraphattentionnetworks_amd.graph import csr_cache, get_csr
     monkeypatch.setenv("GAT_HUB_SEG", "64")
     if slices is not None:
         monkeypatch.setenv("GAT_WH_SLICES", slices)
+    if merge is not None:
+        monkeypatch.setenv("GAT_EDGE_MERGE", merge)
     csr_cache.clear()
     x, ei, state = _hub_case(1500, 30000, [(3, 5000), (700, 1200), (9, 300), (1499, 129),
                                            (0, 2048)], 24, H, F, concat, seed=H * F)
@@ -150,6 +154,19 @@ def test_hub_row_of_120k_edges():
         csr_cache.clear()
     assert_at_least_reference_accuracy(out2, state, x, ei, 8, True)
     torch.testing.assert_close(out2, out, atol=ATOL, rtol=RTOL)
+    # the one-wave merge (GAT_EDGE_MERGE=0) sums the segments in another order
+    os.environ["GAT_EDGE_MERGE"] = "0"
+    try:
+        tuning.reload()
+        csr_cache.clear()
+        eid3 = ei.to(DEV)
+        with torch.no_grad():
+            out3 = layer(x.to(DEV), eid3).cpu()
+    finally:
+        del os.environ["GAT_EDGE_MERGE"]
+        tuning.reload()
+        csr_cache.clear()
+    torch.testing.assert_close(out3, out, atol=1e-6, rtol=1e-6)
 
 
 def test_reddit_powerlaw_sampled_rows():

@@ -75,7 +75,8 @@ def variant(request, monkeypatch):
               "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
               "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
-              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_XPROJ"):
+              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_XPROJ",
+              "GAT_EDGE_MERGE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
