@@ -648,8 +648,11 @@ def emulated_ranks(meas: dict, ranks, exchanges=("allgather",)) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 100 timed steps: the first step's host enqueue and the closing synchronize
+    # (~25-30 us together) are paid once per timed region; over 20 steps they
+    # added ~1.5 us to every 36-us PPI step, over 100 they add ~0.3 us
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="ppi")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as a captured HIP graph (default: eager launches, "
