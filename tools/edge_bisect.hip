@@ -1,0 +1,246 @@
+// PPI edge-kernel bisection: the library's k_edge_grp over a PPI-shaped
+// scheduled CSR (2 column planes, 8 lanes per 128-B plane row, 4 edges per
+// chunk) against probe kernels that keep its memory pattern and add its
+// pieces one at a time, to find where the time beyond the pure gathers goes
+// (tools/line_gather_ceiling: 2-plane random 128-B gathers run at ~21 TB/s of
+// requests; the library kernel at ~12.5 TB/s).
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/edge_bisect.hip \
+//       -Latmlgraphattentionnetworks_amd -lgat_amd \
+//       -Wl,-rpath,'$ORIGIN/../atmlgraphattentionnetworks_amd' -o tools/edge_bisect
+//   tools/edge_bisect                 (prints one JSON object)
+//
+// Probes (one lane group of 8 lanes per (row, plane), workgroup b on plane b % 2):
+//   gather      row bounds by schedule position, col chunk, 4 gathers, sum
+//   gather_pf   + the next chunk's col loads issued before this chunk's gathers
+//   softmax     gather_pf + the fused score, LeakyReLU and online softmax
+//   persist     softmax with each lane group walking several rows (grid-stride),
+//               the next row's bounds loaded during the current row
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../include/gat_amd.h"
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                  \
+        }                                                                             \
+    } while (0)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int G = 8, U = 4, H = 8, F = 8, PW = 32;  // plane width (floats)
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ float pair_sum(float v) {  // sum over lanes l, l ^ 1
+    return v + __shfl_xor(v, 1);
+}
+
+// MODE 0 gather, 1 gather_pf, 2 softmax; PERSIST: grid-stride over positions
+template <int MODE, bool PERSIST>
+__global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const int* __restrict__ se,
+                                               const int* __restrict__ col, int n,
+                                               const float* __restrict__ wh, long long plane_stride,
+                                               const float* __restrict__ a_src,
+                                               const float* __restrict__ s_dst,
+                                               float* __restrict__ out) {
+    const int lane = threadIdx.x & 63, c = lane & (G - 1), gbase = lane & ~(G - 1);
+    const int sl = blockIdx.x & 1;
+    const unsigned blk = blockIdx.x >> 1;
+    const unsigned nblk = gridDim.x >> 1;
+    const int g_first = (int)((blk * 256u + threadIdx.x) / G);
+    const int g_stride = PERSIST ? (int)(nblk * 256u / G) : n;
+    const float* __restrict__ W = wh + sl * plane_stride + 4 * c;
+    const int coff = sl * PW + 4 * c, h = coff / F;
+    const f32x4 a4 = *reinterpret_cast<const f32x4*>(a_src + coff) * kLog2e;
+    int pos = g_first;
+    if (pos >= n) return;
+    int e0 = sb[pos], e1 = se[pos];
+    for (;;) {
+        const int nxt = pos + g_stride;
+        int ne0 = 0, ne1 = 0;
+        if (PERSIST && nxt < n) {  // the next row's bounds, in flight during this row
+            ne0 = sb[nxt];
+            ne1 = se[nxt];
+        }
+        const float sd = s_dst[(size_t)pos * H + h] * kLog2e;
+        float m = -INFINITY, l = 0.f;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        // lane c holds col slot (c & 3) of the chunk
+        int cv = col[min(e0 + (c & 3), e1 - 1)];
+        for (int k = e0; k < e1; k += U) {
+            int cn = 0;
+            if (MODE >= 1) cn = col[min(k + U + (c & 3), e1 - 1)];
+            int j[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) j[u] = __shfl(cv, (lane & ~3) + u);
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const f32x4*>(W + (size_t)j[u] * PW);
+            const int nk = min(U, e1 - k);
+            if (MODE <= 1) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (u < nk) acc += v[u];
+            } else {
+                float s[U];
+                float emax = -INFINITY;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    float d = v[u].x * a4.x + v[u].y * a4.y + v[u].z * a4.z + v[u].w * a4.w;
+                    d = pair_sum(d);
+                    const float z = sd + d;
+                    s[u] = u < nk ? fmaxf(z, z * 0.2f) : -INFINITY;
+                    emax = fmaxf(emax, s[u]);
+                }
+                const float mn = fmaxf(m, emax);
+                const float sc = __builtin_amdgcn_exp2f(m - mn);
+                l *= sc;
+                acc *= sc;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const float p = __builtin_amdgcn_exp2f(s[u] - mn);
+                    l += p;
+                    acc += p * v[u];
+                }
+                m = mn;
+            }
+            if (MODE >= 1) cv = cn;
+            else cv = col[min(k + U + (c & 3), e1 - 1)];
+        }
+        const float inv = MODE == 2 ? 1.f / (l + 1e-16f) : 1.f;
+        *reinterpret_cast<f32x4*>(out + (size_t)pos * 64 + coff) = acc * inv;
+        if (!PERSIST) break;
+        pos = nxt;
+        if (pos >= n) break;
+        e0 = ne0;
+        e1 = ne1;
+    }
+    (void)gbase;
+}
+
+int main() {
+    const int n = 44906;
+    std::mt19937 rng(5);
+    std::vector<int> deg(n);
+    long long E = 0;
+    std::binomial_distribution<int> bd(27 * 4, 0.25);  // ~27 in-edges + the self-loop
+    for (int i = 0; i < n; ++i) {
+        deg[i] = 1 + bd(rng);
+        E += deg[i];
+    }
+    std::sort(deg.begin(), deg.end(), std::greater<int>());  // schedule: descending degree
+    std::vector<int> sb(n), se(n), col(E), order(n);
+    std::uniform_int_distribution<int> ud(0, n - 1);
+    long long p = 0;
+    for (int i = 0; i < n; ++i) {
+        sb[i] = (int)p;
+        for (int k = 0; k < deg[i]; ++k) col[p + k] = ud(rng);
+        std::sort(col.begin() + p, col.begin() + p + deg[i]);
+        p += deg[i];
+        se[i] = (int)p;
+        order[i] = i;
+    }
+    int *d_sb, *d_se, *d_col, *d_order;
+    float *d_wh, *d_a, *d_c, *d_sd, *d_bias, *d_out;
+    CK(hipMalloc(&d_sb, n * 4));
+    CK(hipMalloc(&d_se, n * 4));
+    CK(hipMalloc(&d_order, n * 4));
+    CK(hipMalloc(&d_col, E * 4));
+    CK(hipMalloc(&d_wh, (size_t)n * 64 * 4));
+    CK(hipMalloc(&d_a, 64 * 4));
+    CK(hipMalloc(&d_c, 8 * 4));
+    CK(hipMalloc(&d_sd, (size_t)n * 8 * 4));
+    CK(hipMalloc(&d_bias, 64 * 4));
+    CK(hipMalloc(&d_out, (size_t)n * 64 * 4));
+    CK(hipMemcpy(d_sb, sb.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_se, se.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_order, order.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_col, col.data(), E * 4, hipMemcpyHostToDevice));
+    {
+        std::normal_distribution<float> nd(0.f, 1.f);
+        std::vector<float> t((size_t)n * 64);
+        for (auto& v : t) v = nd(rng) * 0.3f;
+        CK(hipMemcpy(d_wh, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+        std::vector<float> a(64), c(8, 0.1f), sd((size_t)n * 8), b(64, 0.f);
+        for (auto& v : a) v = nd(rng) * 0.3f;
+        for (auto& v : sd) v = nd(rng) * 0.3f;
+        CK(hipMemcpy(d_a, a.data(), 64 * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_c, c.data(), 8 * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_sd, sd.data(), sd.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_bias, b.data(), 64 * 4, hipMemcpyHostToDevice));
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const long long plane_stride = (long long)n * PW;
+    auto time_it = [&](auto&& fn) {
+        for (int i = 0; i < 3; ++i) fn();
+        CK(hipDeviceSynchronize());
+        std::vector<float> v;
+        for (int r = 0; r < 7; ++r) {
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < 20; ++i) fn();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            v.push_back(t * 1e3f / 20);
+        }
+        std::sort(v.begin(), v.end());
+        return v[3];
+    };
+    const int blocks = ((n * G + 255) / 256) * 2;
+    auto lib = [&]() {
+        const int rc = gat_edge_aggregate_seg(d_sb, d_se, 1, d_col, d_order, 0, n, d_wh, PW, n, 2,
+                                              d_a, d_c, d_sd, H, F, 1, 0.2f, nullptr, nullptr, 0, 0,
+                                              d_bias, d_out, (int)(E / n), nullptr);
+        if (rc != 0) {
+            fprintf(stderr, "library rc %d\n", rc);
+            exit(1);
+        }
+    };
+    printf("{\n \"shape\": {\"n\": %d, \"E\": %lld, \"planes\": 2, \"G\": %d, \"U\": %d},\n", n, E, G, U);
+    printf(" \"library_k_edge_grp_us\": %.2f,\n", time_it(lib));
+    fflush(stdout);
+#define PROBE(NAME, MODE, PERS, GRID)                                                            \
+    printf(" \"%s_us\": %.2f,\n", NAME, time_it([&]() {                                         \
+               hipLaunchKernelGGL((k_probe<MODE, PERS>), dim3(GRID), dim3(256), 0, 0, d_sb, d_se, \
+                                  d_col, n, d_wh, plane_stride, d_a, d_sd, d_out);               \
+           }));                                                                                  \
+    fflush(stdout);
+    PROBE("gather", 0, false, blocks)
+    PROBE("gather_pf", 1, false, blocks)
+    PROBE("softmax", 2, false, blocks)
+    PROBE("persist_24w", 2, true, 1536)
+    PROBE("persist_32w", 2, true, 2048)
+    PROBE("gather_persist_32w", 1, true, 2048)
+    // the same rows with their sources in random order (the multiset of each
+    // row unchanged): does the ascending-source walk help or hurt?
+    {
+        std::vector<int> colr = col;
+        for (int i = 0; i < n; ++i) std::shuffle(colr.begin() + sb[i], colr.begin() + se[i], rng);
+        CK(hipMemcpy(d_col, colr.data(), E * 4, hipMemcpyHostToDevice));
+        printf(" \"unsorted_library_k_edge_grp_us\": %.2f,\n", time_it(lib));
+        PROBE("unsorted_gather", 0, false, blocks)
+        PROBE("unsorted_gather_pf", 1, false, blocks)
+        // every row's sources uniformly random over the whole table AND rows
+        // independent of each other: a fresh random multiset (unsorted)
+        std::vector<int> colu(E);
+        for (auto& v : colu) v = ud(rng);
+        CK(hipMemcpy(d_col, colu.data(), E * 4, hipMemcpyHostToDevice));
+        PROBE("fresh_random_gather_pf", 1, false, blocks)
+        CK(hipMemcpy(d_col, col.data(), E * 4, hipMemcpyHostToDevice));
+    }
+    const double req = (double)E * 2 * 128;
+    printf(" \"request_bytes\": %.0f\n}\n", req);
+    return 0;
+}
