@@ -16,7 +16,7 @@ static const char* const kKnobNames[] = {
     "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS", "GAT_BWD_KINK",
     "GAT_WGRAD_LW",    "GAT_STORE_WT",    "GAT_PROJ_WK_DIRECT", "GAT_EDGE_SPLIT",
     "GAT_PROJ_X3V",    "GAT_PROJ_WG",     "GAT_EDGE_LDSDMA", "GAT_PROJ_PRESPLIT", "GAT_BWD_SL",
-    "GAT_EDGE_HL",     "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_XPROJ", "GAT_EDGE_MERGE"};
+    "GAT_EDGE_HL",     "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_XPROJ", "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL"};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {

@@ -227,8 +227,15 @@ struct XRow {  // one x row of the small-Fin form: N floats, 4-B aligned
     float v[N];
 };
 
+// RC (> 0; U = 4, quad-broadcast ids, S = 1, not PIPE): a row's col values are
+// loaded 8 chunks at a time, one load per lane and register for 8 / (G / 4)
+// chunks (chunk t's four ids in quad t % (G/4) of the group), instead of one
+// chunk ahead: the col stream comes from HBM, and its per-chunk round trip
+// was the walk's critical path at short rows (tools/edge_bisect.hip: a
+// memory-only PPI walk 24.4 -> 21.4 us).  Same chunks, ids and order:
+// results are bitwise the one-chunk-ahead form's.
 template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1,
-          int HL = 0, int XF = 0>
+          int HL = 0, int XF = 0, int RC = 0>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -242,6 +249,7 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     const DropArgs drop = resolve_drop(drop_arg);
     static_assert(S == 1 || ((S == 2 || S == 4) && !KINK && !PIPE && G * S <= kWave), "split rows");
     static_assert(XF == 0 || (V == 1 && FUSED && !KINK && !PIPE && S == 1), "small-Fin form");
+    static_assert(RC == 0 || (U == 4 && G >= 4 && S == 1 && !PIPE), "row-batched col values");
     // col values held per lane per chunk.  Groups of >= 4 lanes: every quad of
     // the group holds the chunk's indices (lane c: edges (c & 3) + 4t), so the
     // source ids are broadcast by DPP within the quad instead of LDS permutes
@@ -540,6 +548,28 @@ __global__ __launch_bounds__(256) void k_edge_grp(
             if (k + U < e1) consume(k + U, vb, sb);
 #pragma unroll
             for (int t = 0; t < CL; ++t) cb[t] = cb2[t];
+        }
+    } else if constexpr (RC > 0) {
+        // ids of up to 8 chunks per round trip (see RC above)
+        constexpr int NQ = G / 4, R = 8 / NQ > 0 ? 8 / NQ : 1, NB = NQ * R;
+        const int qd = (c >> 2) & (NQ - 1), pq = c & 3;
+        for (int b0 = e0; b0 < e1; b0 += NB * U) {
+            int cr[R];
+#pragma unroll
+            for (int q = 0; q < R; ++q) cr[q] = col[min(b0 + U * (NQ * q + qd) + pq, e1 - 1)];
+#pragma unroll
+            for (int t = 0; t < NB; ++t) {
+                const int k = b0 + U * t;
+                if (k >= e1) break;
+                int cc[CL];
+                // chunk t's ids into this lane's quad (then broadcast inside it)
+                if constexpr (NQ == 1) cc[0] = cr[t];
+                else cc[0] = __shfl(cr[t / NQ], gbase + 4 * (t % NQ) + pq);
+                f32x4 v[U][V];
+                float s[U];
+                fetch(cc, v, s);
+                consume(k, v, s);
+            }
         }
     } else {
         for (int k = e0 + half * U; k < e1; k += S * U) {
@@ -965,8 +995,41 @@ __global__ __launch_bounds__(256) void k_edge_merge_wg(
 // lane group is one of HF = 64's (G = 4, 8, 16: planes or rows, V = 1 or 2)
 // and hl is 1 or 2 (heads of 4 or 8 columns); the run-time form otherwise.
 // GAT_EDGE_HL=0 (A/B knob) forces the run-time form.
+// The row-batched col form (RC) for rows of >= 16 in-edges on average (PPI:
+// edge kernel 26.3 -> 25.2 us, same box, profiles/r05/edge_ab_rowcol_ppi.json);
+// rows of 2-3 chunks (arxiv, CIFAR) keep the one-chunk-ahead loads, which
+// there measured faster (arxiv 54.0 vs 55.9 us, CIFAR H=8 18.8 vs 20.2;
+// profiles/r05/edge_ab_rowcol_ungated_*.json).
+// GAT_EDGE_ROWCOL=0 (A/B knob): never.
+static bool rowcol_for(int edges_per_row_hint) {
+    const char* v = knob("GAT_EDGE_ROWCOL");
+    return (v == nullptr || std::atoi(v) != 0) && edges_per_row_hint >= 16;
+}
+
 template <int G, int U, int V, bool PIPE, bool KINK, int S, class... A>
-static void launch_grp_hl(int hl, dim3 grid, dim3 block, size_t lds, hipStream_t st, A... a) {
+static void launch_grp_hl(int hl, bool rc, dim3 grid, dim3 block, size_t lds, hipStream_t st,
+                          A... a) {
+    if constexpr (U == 4 && G >= 4 && S == 1 && !PIPE) {
+        if (rc) {
+            if constexpr (G == 4 || G == 8 || G == 16) {
+                const char* v = knob("GAT_EDGE_HL");
+                const bool on = v == nullptr || std::atoi(v) != 0;
+                if (on && hl == 1) {
+                    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1, 0, 1>), grid,
+                                       block, lds, st, a...);
+                    return;
+                }
+                if (on && hl == 2) {
+                    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 2, 0, 1>), grid,
+                                       block, lds, st, a...);
+                    return;
+                }
+            }
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 0, 0, 1>), grid, block,
+                               lds, st, a...);
+            return;
+        }
+    }
     if constexpr (G == 4 || G == 8 || G == 16) {
         const char* v = knob("GAT_EDGE_HL");
         const bool on = v == nullptr || std::atoi(v) != 0;
@@ -983,8 +1046,8 @@ static void launch_grp_hl(int hl, dim3 grid, dim3 block, size_t lds, hipStream_t
 }
 
 template <int G, int U, int V, bool KINK = false, class... A>
-static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block, hipStream_t st,
-                              A... a) {
+static void launch_edge_fused(int pipe, int split, int hl, bool rc, dim3 grid, dim3 block,
+                              hipStream_t st, A... a) {
     // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
     // kernel — caps the blocks resident per CU (160 KB / bytes)
     size_t lds = 0;
@@ -996,7 +1059,7 @@ static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block
     // 54.0 -> 54.9 us, CIFAR equal; profiles/r05/edge_ab_pipe_short_*.json)
     if constexpr (V == 2 && (U == 16 || U == 8)) {
         if (pipe) {
-            launch_grp_hl<G, U, V, true, KINK, 1>(hl, grid, block, lds, st, a...);
+            launch_grp_hl<G, U, V, true, KINK, 1>(hl, rc, grid, block, lds, st, a...);
             return;
         }
     }
@@ -1005,24 +1068,28 @@ static void launch_edge_fused(int pipe, int split, int hl, dim3 grid, dim3 block
     // row-major)
     if constexpr (!KINK && V == 1 && U <= 8 && (G == 8 || G == 16)) {
         if (split == 2) {
-            launch_grp_hl<G, U, V, false, false, 2>(hl, dim3(grid.x * 2), block, lds, st, a...);
+            launch_grp_hl<G, U, V, false, false, 2>(hl, rc, dim3(grid.x * 2), block, lds, st, a...);
             return;
         }
         if (split == 4) {
-            launch_grp_hl<G, U, V, false, false, 4>(hl, dim3(grid.x * 4), block, lds, st, a...);
+            launch_grp_hl<G, U, V, false, false, 4>(hl, rc, dim3(grid.x * 4), block, lds, st, a...);
             return;
         }
     }
-    launch_grp_hl<G, U, V, false, KINK, 1>(hl, grid, block, lds, st, a...);
+    launch_grp_hl<G, U, V, false, KINK, 1>(hl, rc, grid, block, lds, st, a...);
 }
 
 // the small-Fin fused forward (XF): lane groups of HF = 32 or 64 (G = 8, 16),
 // heads of 4 or 8 columns, U = 4 or 8, fin 1-4
 template <int G, int U, int HL, class... A>
-static void launch_xf_fin(int xf, dim3 grid, dim3 block, hipStream_t st, A... a) {
+static void launch_xf_fin(int xf, bool rc, dim3 grid, dim3 block, hipStream_t st, A... a) {
 #define GAT_XF(N)                                                                               \
-    hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, N>), grid, block,        \
-                       0, st, a...)
+    if (U == 4 && rc)                                                                           \
+        hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, N, U == 4 ? 1 : 0>), \
+                           grid, block, 0, st, a...);                                           \
+    else                                                                                        \
+        hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, N>), grid, block,    \
+                           0, st, a...)
     switch (xf) {
         case 1: GAT_XF(1); break;
         case 2: GAT_XF(2); break;
@@ -1033,13 +1100,14 @@ static void launch_xf_fin(int xf, dim3 grid, dim3 block, hipStream_t st, A... a)
 }
 
 template <int G, class... A>
-static void launch_xf(int u, int hl, int xf, dim3 grid, dim3 block, hipStream_t st, A... a) {
+static void launch_xf(int u, int hl, int xf, bool rc, dim3 grid, dim3 block, hipStream_t st,
+                      A... a) {
     if (u == 4) {
-        if (hl == 1) launch_xf_fin<G, 4, 1>(xf, grid, block, st, a...);
-        else launch_xf_fin<G, 4, 2>(xf, grid, block, st, a...);
+        if (hl == 1) launch_xf_fin<G, 4, 1>(xf, rc, grid, block, st, a...);
+        else launch_xf_fin<G, 4, 2>(xf, rc, grid, block, st, a...);
     } else {
-        if (hl == 1) launch_xf_fin<G, 8, 1>(xf, grid, block, st, a...);
-        else launch_xf_fin<G, 8, 2>(xf, grid, block, st, a...);
+        if (hl == 1) launch_xf_fin<G, 8, 1>(xf, false, grid, block, st, a...);
+        else launch_xf_fin<G, 8, 2>(xf, false, grid, block, st, a...);
     }
 }
 
@@ -1048,9 +1116,10 @@ static void launch_xf(int u, int hl, int xf, dim3 grid, dim3 block, hipStream_t 
 static bool kink_grp_ok(int g, int v) { return (g == 16 && v == 1) || (g == 8 && v == 2); }
 
 template <int G, int U, int V, class... A>
-static void launch_edge_kink(int pipe, int hl, dim3 grid, dim3 block, hipStream_t st, A... a) {
+static void launch_edge_kink(int pipe, int hl, bool rc, dim3 grid, dim3 block, hipStream_t st,
+                             A... a) {
     if constexpr ((G == 16 && V == 1) || (G == 8 && V == 2))
-        launch_edge_fused<G, U, V, true>(pipe, 1, hl, grid, block, st, a...);
+        launch_edge_fused<G, U, V, true>(pipe, 1, hl, rc, grid, block, st, a...);
 }
 
 extern "C" {
@@ -1196,6 +1265,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         if (kink || pipe) split = 1;
         if ((long long)blocks * split >= (1LL << 31)) split = 1;
         if (kink && !kink_grp_ok(g, vv)) return GAT_EUNSUPPORTED;
+        const bool rc = rowcol_for(edges_per_row_hint);
         const XProjArgs xpa = xp != nullptr ? *xp : XProjArgs{nullptr, nullptr, nullptr, nullptr,
                                                               nullptr, 0};
 #define GAT_GRP_KARGS                                                                         \
@@ -1210,15 +1280,15 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
                   xp->a_dst != nullptr && xp->c_dst != nullptr))
                 return GAT_EUNSUPPORTED;
             const int xf = xp->fin;
-            if (g == 8) launch_xf<8>(u, hl, xf, grid, block, st, GAT_GRP_KARGS);
-            else launch_xf<16>(u, hl, xf, grid, block, st, GAT_GRP_KARGS);
+            if (g == 8) launch_xf<8>(u, hl, xf, rc, grid, block, st, GAT_GRP_KARGS);
+            else launch_xf<16>(u, hl, xf, rc, grid, block, st, GAT_GRP_KARGS);
             return status_of(hipGetLastError());
         }
 #define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
     if (kink)                                                                         \
-        launch_edge_kink<G, UU, VV>(pipe, hl, grid, block, st, GAT_GRP_KARGS);         \
+        launch_edge_kink<G, UU, VV>(pipe, hl, rc, grid, block, st, GAT_GRP_KARGS);     \
     else if (fused)                                                                   \
-        launch_edge_fused<G, UU, VV>(pipe, split, hl, grid, block, st, GAT_GRP_KARGS); \
+        launch_edge_fused<G, UU, VV>(pipe, split, hl, rc, grid, block, st, GAT_GRP_KARGS); \
     else                                                                              \
         hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, GAT_GRP_KARGS)
 #define GAT_GRP_U(G, VV)                                                              \

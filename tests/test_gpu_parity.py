@@ -39,6 +39,8 @@ VARIANTS = {
     # Fin <= 4: projection and edge kernel as two launches instead of the fused
     # small-Fin kernel (the default through gat_layer_forward)
     "no_xproj": {"GAT_EDGE_XPROJ": "0"},
+    # short-row col values one chunk ahead instead of 8 chunks per load
+    "no_rowcol": {"GAT_EDGE_ROWCOL": "0"},
     "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
     "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds", "GAT_EDGE_SCHED": "0"},
     # the CSR-order launch (short rows take the scheduled copy by default)
@@ -76,7 +78,7 @@ def variant(request, monkeypatch):
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
               "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
               "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_XPROJ",
-              "GAT_EDGE_MERGE"):
+              "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -167,6 +169,35 @@ def test_random_vs_oracle(case, variant):
     ref = gat_layer_forward_from_state(state, x, ei, H, concat)
     out = run_layer(layer_from_state(state, fin, F, H, concat), x, ei)
     torch.testing.assert_close(out, ref, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.parametrize("n,e,fin,H,F,concat,kind", [
+    (3000, 84000, 50, 8, 8, True, "uniform"),    # PPI-like rows, 2 column planes, G = 8
+    (5000, 40000, 128, 8, 8, True, "uniform"),   # arxiv-like rows: not row-batched (< 16)
+    (2000, 30000, 20, 8, 8, False, "uniform"),   # head mean, row-major, G = 16
+    (1500, 30000, 3, 4, 8, True, "uniform"),     # small Fin: the fused projection
+    (1500, 60000, 24, 2, 16, True, "hub"),       # a hub row split into segments, U = 8
+])
+def test_rowcol_bitwise(n, e, fin, H, F, concat, kind, monkeypatch):
+    """Col values loaded 8 chunks per round trip (k_edge_grp RC, the default at
+    U = 4 for rows of >= 16 in-edges on average) walk the same chunks with the
+    same ids in the same order as the one-chunk-ahead form (GAT_EDGE_ROWCOL=0):
+    bitwise equal outputs."""
+    from atmlgraphattentionnetworks_amd import tuning
+    from atmlgraphattentionnetworks_amd.graph import csr_cache
+    x, ei, state = random_case(n, e, fin, H, F, concat, seed=n + fin, kind=kind)
+    outs = []
+    for env in ({}, {"GAT_EDGE_ROWCOL": "0"}):
+        monkeypatch.delenv("GAT_EDGE_ROWCOL", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        tuning.reload()
+        csr_cache.clear()
+        outs.append(run_layer(layer_from_state(state, fin, F, H, concat), x, ei))
+    csr_cache.clear()
+    assert torch.equal(outs[0], outs[1])
+    ref = gat_layer_forward_from_state(state, x, ei, H, concat)
+    torch.testing.assert_close(outs[0], ref, atol=ATOL, rtol=RTOL)
 
 
 def test_edge_order_invariance_and_determinism():

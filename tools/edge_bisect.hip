@@ -44,7 +44,10 @@ __device__ __forceinline__ float pair_sum(float v) {  // sum over lanes l, l ^ 1
     return v + __shfl_xor(v, 1);
 }
 
-// MODE 0 gather, 1 gather_pf, 2 softmax; PERSIST: grid-stride over positions
+// MODE 0 gather, 1 gather_pf, 2 softmax, 3 gather_pf without the output store
+// (kept only for a sentinel value), 4 gather_pf with hashed source ids (no col
+// stream), 5 gathers with each row's col values loaded 8 chunks at a time;
+// PERSIST: grid-stride over positions
 template <int MODE, bool PERSIST>
 __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const int* __restrict__ se,
                                                const int* __restrict__ col, int n,
@@ -74,11 +77,48 @@ __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const
         const float sd = s_dst[(size_t)pos * H + h] * kLog2e;
         float m = -INFINITY, l = 0.f;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == 5) {
+            // the row's col values for 8 chunks at a time, loaded at once: chunk t's
+            // 4 ids sit in quad (t & 1) of the group, register t >> 1
+            const int q = (c >> 2) & 1, pq = c & 3;
+            for (int b0 = e0; b0 < e1; b0 += 8 * U) {
+                int cr[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) cr[r] = col[min(b0 + U * (2 * r + q) + pq, e1 - 1)];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int k = b0 + U * t;
+                    if (k >= e1) break;
+                    int j[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) j[u] = __shfl(cr[t >> 1], gbase + 4 * (t & 1) + u);
+                    f32x4 v[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        v[u] = *reinterpret_cast<const f32x4*>(W + (size_t)j[u] * PW);
+                    const int nk = min(U, e1 - k);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (u < nk) acc += v[u];
+                }
+            }
+            *reinterpret_cast<f32x4*>(out + (size_t)pos * 64 + coff) = acc;
+            if (!PERSIST) break;
+            pos = nxt;
+            if (pos >= n) break;
+            e0 = ne0;
+            e1 = ne1;
+            continue;
+        }
         // lane c holds col slot (c & 3) of the chunk
-        int cv = col[min(e0 + (c & 3), e1 - 1)];
+        int cv = MODE == 4 ? (int)(((unsigned)(e0 + (c & 3)) * 2654435761u >> 7) % (unsigned)n)
+                           : col[min(e0 + (c & 3), e1 - 1)];
         for (int k = e0; k < e1; k += U) {
             int cn = 0;
-            if (MODE >= 1) cn = col[min(k + U + (c & 3), e1 - 1)];
+            if (MODE == 4)
+                cn = (int)(((unsigned)(k + U + (c & 3)) * 2654435761u >> 7) % (unsigned)n);
+            else if (MODE >= 1)
+                cn = col[min(k + U + (c & 3), e1 - 1)];
             int j[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) j[u] = __shfl(cv, (lane & ~3) + u);
@@ -86,7 +126,7 @@ __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const
 #pragma unroll
             for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const f32x4*>(W + (size_t)j[u] * PW);
             const int nk = min(U, e1 - k);
-            if (MODE <= 1) {
+            if (MODE != 2) {
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (u < nk) acc += v[u];
@@ -117,7 +157,8 @@ __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const
             else cv = col[min(k + U + (c & 3), e1 - 1)];
         }
         const float inv = MODE == 2 ? 1.f / (l + 1e-16f) : 1.f;
-        *reinterpret_cast<f32x4*>(out + (size_t)pos * 64 + coff) = acc * inv;
+        if (MODE != 3 || acc.x == 12345.f)
+            *reinterpret_cast<f32x4*>(out + (size_t)pos * 64 + coff) = acc * inv;
         if (!PERSIST) break;
         pos = nxt;
         if (pos >= n) break;
@@ -223,6 +264,10 @@ int main() {
     PROBE("persist_24w", 2, true, 1536)
     PROBE("persist_32w", 2, true, 2048)
     PROBE("gather_persist_32w", 1, true, 2048)
+    PROBE("gather_pf_nostore", 3, false, blocks)
+    PROBE("gather_pf_hashcol", 4, false, blocks)
+    PROBE("gather_rowcol", 5, false, blocks)
+    PROBE("gather_rowcol_persist_32w", 5, true, 2048)
     // the same rows with their sources in random order (the multiset of each
     // row unchanged): does the ascending-source walk help or hurt?
     {
