@@ -177,6 +177,7 @@ def test_random_vs_oracle(case, variant):
     (2000, 30000, 20, 8, 8, False, "uniform"),   # head mean, row-major, G = 16
     (1500, 30000, 3, 4, 8, True, "uniform"),     # small Fin: the fused projection
     (1500, 60000, 24, 2, 16, True, "hub"),       # a hub row split into segments, U = 8
+    (2000, 400000, 24, 8, 8, True, "uniform"),   # ~200 per row: pipelined, not row-batched
 ])
 def test_rowcol_bitwise(n, e, fin, H, F, concat, kind, monkeypatch):
     """Col values loaded 8 chunks per round trip (k_edge_grp RC, the default at
@@ -196,8 +197,35 @@ def test_rowcol_bitwise(n, e, fin, H, F, concat, kind, monkeypatch):
         outs.append(run_layer(layer_from_state(state, fin, F, H, concat), x, ei))
     csr_cache.clear()
     assert torch.equal(outs[0], outs[1])
-    ref = gat_layer_forward_from_state(state, x, ei, H, concat)
-    torch.testing.assert_close(outs[0], ref, atol=ATOL, rtol=RTOL)
+    if kind == "uniform":  # (a 30k-200k-edge hub row: tests/test_gpu_hubs.py's bar)
+        ref = gat_layer_forward_from_state(state, x, ei, H, concat)
+        torch.testing.assert_close(outs[0], ref, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.parametrize("n,e", [(3000, 84000)])
+def test_rowcol_training_bitwise(n, e, monkeypatch):
+    """The training forward (kink sums, k_edge_grp KINK) with the row-batched
+    ids (PPI-like rows) against the one-chunk-ahead form: outputs and input
+    gradients bitwise equal (no dropout, so both runs draw nothing)."""
+    from atmlgraphattentionnetworks_amd import tuning
+    from atmlgraphattentionnetworks_amd.graph import csr_cache
+    x, ei, state = random_case(n, e, 24, 8, 8, True, seed=n, kind="uniform")
+    g = torch.randn(n, 64, generator=torch.Generator().manual_seed(3))
+    res = []
+    for env in ({}, {"GAT_EDGE_ROWCOL": "0"}):
+        monkeypatch.delenv("GAT_EDGE_ROWCOL", raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        tuning.reload()
+        csr_cache.clear()
+        layer = layer_from_state(state, 24, 8, 8, True)
+        xd = x.to(dev()).requires_grad_(True)
+        y = layer(xd, ei.to(dev()))
+        y.backward(g.to(dev()))
+        res.append((y.detach().cpu(), xd.grad.cpu()))
+    csr_cache.clear()
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
 
 
 def test_edge_order_invariance_and_determinism():
