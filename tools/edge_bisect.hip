@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <functional>
 #include <cstdlib>
 #include <random>
 #include <vector>
@@ -36,6 +37,7 @@
     } while (0)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int G = 8, U = 4, H = 8, F = 8, PW = 32;  // plane width (floats)
 constexpr float kLog2e = 1.4426950408889634f;
@@ -46,15 +48,16 @@ __device__ __forceinline__ float pair_sum(float v) {  // sum over lanes l, l ^ 1
 
 // MODE 0 gather, 1 gather_pf, 2 softmax, 3 gather_pf without the output store
 // (kept only for a sentinel value), 4 gather_pf with hashed source ids (no col
-// stream), 5 gathers with each row's col values loaded 8 chunks at a time;
-// PERSIST: grid-stride over positions
+// stream), 5 gathers with each row's col values loaded 8 chunks at a time,
+// 6 = 5 + the softmax, 7 = 6 with write-through output stores, 8 = 6 with the
+// target row read through the order array; PERSIST: grid-stride over positions
 template <int MODE, bool PERSIST>
 __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const int* __restrict__ se,
                                                const int* __restrict__ col, int n,
                                                const float* __restrict__ wh, long long plane_stride,
                                                const float* __restrict__ a_src,
                                                const float* __restrict__ s_dst,
-                                               float* __restrict__ out) {
+                                               float* __restrict__ out, const int* __restrict__ order) {
     const int lane = threadIdx.x & 63, c = lane & (G - 1), gbase = lane & ~(G - 1);
     const int sl = blockIdx.x & 1;
     const unsigned blk = blockIdx.x >> 1;
@@ -77,10 +80,14 @@ __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const
         const float sd = s_dst[(size_t)pos * H + h] * kLog2e;
         float m = -INFINITY, l = 0.f;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (MODE == 5) {
+        if constexpr (MODE >= 5) {
             // the row's col values for 8 chunks at a time, loaded at once: chunk t's
             // 4 ids sit in quad (t & 1) of the group, register t >> 1
             const int q = (c >> 2) & 1, pq = c & 3;
+            // MODE 8: target row through the order array (identity here), as the
+            // library's scheduled CSR reads s_dst[order[pos]]
+            const int orow = MODE == 8 ? order[pos] : pos;
+            const float sdr = MODE == 8 ? s_dst[(size_t)orow * H + h] * kLog2e : sd;
             for (int b0 = e0; b0 < e1; b0 += 8 * U) {
                 int cr[4];
 #pragma unroll
@@ -97,12 +104,44 @@ __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const
                     for (int u = 0; u < U; ++u)
                         v[u] = *reinterpret_cast<const f32x4*>(W + (size_t)j[u] * PW);
                     const int nk = min(U, e1 - k);
+                    if constexpr (MODE == 5) {
 #pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        if (u < nk) acc += v[u];
+                        for (int u = 0; u < U; ++u)
+                            if (u < nk) acc += v[u];
+                    } else {
+                        float s[U];
+                        float emax = -INFINITY;
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            float d = v[u].x * a4.x + v[u].y * a4.y + v[u].z * a4.z + v[u].w * a4.w;
+                            d = pair_sum(d);
+                            const float z = sdr + d;
+                            s[u] = u < nk ? fmaxf(z, z * 0.2f) : -INFINITY;
+                            emax = fmaxf(emax, s[u]);
+                        }
+                        const float mn = fmaxf(m, emax);
+                        const float sc = __builtin_amdgcn_exp2f(m - mn);
+                        l *= sc;
+                        acc *= sc;
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const float p = __builtin_amdgcn_exp2f(s[u] - mn);
+                            l += p;
+                            acc += p * v[u];
+                        }
+                        m = mn;
+                    }
                 }
             }
-            *reinterpret_cast<f32x4*>(out + (size_t)pos * 64 + coff) = acc;
+            if constexpr (MODE >= 6) acc *= 1.f / (l + 1e-16f);
+            if constexpr (MODE == 7) {
+                // write-through 16-B store, as the library's store_out4
+                const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7FFFFFFF, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc), rsrc,
+                                                       (int)(((size_t)orow * 64 + coff) * 4), 0, 16);
+            } else {
+                *reinterpret_cast<f32x4*>(out + (size_t)orow * 64 + coff) = acc;
+            }
             if (!PERSIST) break;
             pos = nxt;
             if (pos >= n) break;
@@ -223,67 +262,75 @@ int main() {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const long long plane_stride = (long long)n * PW;
-    auto time_it = [&](auto&& fn) {
-        for (int i = 0; i < 3; ++i) fn();
-        CK(hipDeviceSynchronize());
-        std::vector<float> v;
-        for (int r = 0; r < 7; ++r) {
-            CK(hipEventRecord(e0, 0));
-            for (int i = 0; i < 20; ++i) fn();
-            CK(hipEventRecord(e1, 0));
-            CK(hipEventSynchronize(e1));
-            float t;
-            CK(hipEventElapsedTime(&t, e0, e1));
-            v.push_back(t * 1e3f / 20);
-        }
-        std::sort(v.begin(), v.end());
-        return v[3];
-    };
-    const int blocks = ((n * G + 255) / 256) * 2;
-    auto lib = [&]() {
-        const int rc = gat_edge_aggregate_seg(d_sb, d_se, 1, d_col, d_order, 0, n, d_wh, PW, n, 2,
-                                              d_a, d_c, d_sd, H, F, 1, 0.2f, nullptr, nullptr, 0, 0,
-                                              d_bias, d_out, (int)(E / n), nullptr);
-        if (rc != 0) {
-            fprintf(stderr, "library rc %d\n", rc);
-            exit(1);
-        }
-    };
-    printf("{\n \"shape\": {\"n\": %d, \"E\": %lld, \"planes\": 2, \"G\": %d, \"U\": %d},\n", n, E, G, U);
-    printf(" \"library_k_edge_grp_us\": %.2f,\n", time_it(lib));
-    fflush(stdout);
-#define PROBE(NAME, MODE, PERS, GRID)                                                            \
-    printf(" \"%s_us\": %.2f,\n", NAME, time_it([&]() {                                         \
-               hipLaunchKernelGGL((k_probe<MODE, PERS>), dim3(GRID), dim3(256), 0, 0, d_sb, d_se, \
-                                  d_col, n, d_wh, plane_stride, d_a, d_sd, d_out);               \
-           }));                                                                                  \
-    fflush(stdout);
-    PROBE("gather", 0, false, blocks)
-    PROBE("gather_pf", 1, false, blocks)
-    PROBE("softmax", 2, false, blocks)
-    PROBE("persist_24w", 2, true, 1536)
-    PROBE("persist_32w", 2, true, 2048)
-    PROBE("gather_persist_32w", 1, true, 2048)
-    PROBE("gather_pf_nostore", 3, false, blocks)
-    PROBE("gather_pf_hashcol", 4, false, blocks)
-    PROBE("gather_rowcol", 5, false, blocks)
-    PROBE("gather_rowcol_persist_32w", 5, true, 2048)
-    // the same rows with their sources in random order (the multiset of each
-    // row unchanged): does the ascending-source walk help or hurt?
+    // the same rows with their sources in random order (each row's multiset
+    // unchanged), and fresh uniformly random sources (unsorted)
+    int *d_colr, *d_colu;
+    CK(hipMalloc(&d_colr, E * 4));
+    CK(hipMalloc(&d_colu, E * 4));
     {
         std::vector<int> colr = col;
         for (int i = 0; i < n; ++i) std::shuffle(colr.begin() + sb[i], colr.begin() + se[i], rng);
-        CK(hipMemcpy(d_col, colr.data(), E * 4, hipMemcpyHostToDevice));
-        printf(" \"unsorted_library_k_edge_grp_us\": %.2f,\n", time_it(lib));
-        PROBE("unsorted_gather", 0, false, blocks)
-        PROBE("unsorted_gather_pf", 1, false, blocks)
-        // every row's sources uniformly random over the whole table AND rows
-        // independent of each other: a fresh random multiset (unsorted)
+        CK(hipMemcpy(d_colr, colr.data(), E * 4, hipMemcpyHostToDevice));
         std::vector<int> colu(E);
         for (auto& v : colu) v = ud(rng);
-        CK(hipMemcpy(d_col, colu.data(), E * 4, hipMemcpyHostToDevice));
-        PROBE("fresh_random_gather_pf", 1, false, blocks)
-        CK(hipMemcpy(d_col, col.data(), E * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_colu, colu.data(), E * 4, hipMemcpyHostToDevice));
+    }
+    const int blocks = ((n * G + 255) / 256) * 2;
+    std::vector<std::pair<const char*, std::function<void()>>> vars;
+    auto lib_on = [&](const int* cp) {
+        return [=]() {
+            const int rc = gat_edge_aggregate_seg(d_sb, d_se, 1, cp, d_order, 0, n, d_wh, PW, n, 2,
+                                                  d_a, d_c, d_sd, H, F, 1, 0.2f, nullptr, nullptr,
+                                                  0, 0, d_bias, d_out, (int)(E / n), nullptr);
+            if (rc != 0) {
+                fprintf(stderr, "library rc %d\n", rc);
+                exit(1);
+            }
+        };
+    };
+    vars.push_back({"library_k_edge_grp", lib_on(d_col)});
+#define PROBE(NAME, MODE, PERS, GRID, CP)                                                         \
+    vars.push_back({NAME, [=]() {                                                                 \
+                        hipLaunchKernelGGL((k_probe<MODE, PERS>), dim3(GRID), dim3(256), 0, 0,     \
+                                           d_sb, d_se, CP, n, d_wh, plane_stride, d_a, d_sd,        \
+                                           d_out, d_order);                                         \
+                    }});
+    PROBE("gather", 0, false, blocks, d_col)
+    PROBE("gather_pf", 1, false, blocks, d_col)
+    PROBE("softmax", 2, false, blocks, d_col)
+    PROBE("persist_24w", 2, true, 1536, d_col)
+    PROBE("gather_persist_32w", 1, true, 2048, d_col)
+    PROBE("gather_pf_nostore", 3, false, blocks, d_col)
+    PROBE("gather_pf_hashcol", 4, false, blocks, d_col)
+    PROBE("gather_rowcol", 5, false, blocks, d_col)
+    PROBE("softmax_rowcol", 6, false, blocks, d_col)
+    PROBE("softmax_rowcol_wtstore", 7, false, blocks, d_col)
+    PROBE("softmax_rowcol_order", 8, false, blocks, d_col)
+    vars.push_back({"unsorted_library_k_edge_grp", lib_on(d_colr)});
+    PROBE("unsorted_gather_pf", 1, false, blocks, d_colr)
+    PROBE("fresh_random_gather_pf", 1, false, blocks, d_colu)
+    // interleaved rounds: every variant timed once per round (20 launches), medians
+    std::vector<std::vector<float>> t(vars.size());
+    for (auto& v : vars)
+        for (int i = 0; i < 3; ++i) v.second();
+    CK(hipDeviceSynchronize());
+    for (int r = 0; r < 11; ++r) {
+        for (size_t k = 0; k < vars.size(); ++k) {
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < 20; ++i) vars[k].second();
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            t[k].push_back(ms * 1e3f / 20);
+        }
+    }
+    printf("{\n \"shape\": {\"n\": %d, \"E\": %lld, \"planes\": 2, \"G\": %d, \"U\": %d},\n",
+           n, E, G, U);
+    printf(" \"note\": \"median us of 11 interleaved rounds of 20 launches each\",\n");
+    for (size_t k = 0; k < vars.size(); ++k) {
+        std::sort(t[k].begin(), t[k].end());
+        printf(" \"%s_us\": %.2f,\n", vars[k].first, t[k][5]);
     }
     const double req = (double)E * 2 * 128;
     printf(" \"request_bytes\": %.0f\n}\n", req);
