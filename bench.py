@@ -210,16 +210,21 @@ def cpu_baseline(state, x, ei, heads, concat, n_edges, threads, budget_s=4.0,
 # ---------------------------------------------------------------------------
 # GPU measurement of one single-GPU workload
 # ---------------------------------------------------------------------------
-def _events_ms(fn, iters: int, stream) -> float:
+def _events_ms(fn, iters: int, stream, rounds: int = 1) -> float:
     """Mean time of fn over iters, HIP events recorded on `stream` (the stream
-    the library launches on: torch's current stream)."""
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(iters):
-        fn()
-    ev1.record(stream)
-    ev1.synchronize()
-    return ev0.elapsed_time(ev1) / iters
+    the library launches on: torch's current stream); with rounds > 1 the
+    median of that many such means (one slow round — a clock ramp, another
+    process on the host — does not set the roofline's kernel time)."""
+    means = []
+    for _ in range(rounds):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _ in range(iters):
+            fn()
+        ev1.record(stream)
+        ev1.synchronize()
+        means.append(ev0.elapsed_time(ev1) / iters)
+    return statistics.median(means)
 
 
 def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
@@ -290,14 +295,15 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
         plan.project(lib, x, pp)
         for _ in range(3):
             plan.edge(lib, csr, pp, bias, out)
-        edge_ms = _events_ms(lambda: plan.edge(lib, csr, pp, bias, out), edge_iters, stream)
+        edge_ms = _events_ms(lambda: plan.edge(lib, csr, pp, bias, out), edge_iters, stream,
+                             rounds=5)
         # projection alone: a short kernel, so launches captured in a graph
         gp = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gp):
             for _ in range(edge_iters):
                 plan.project(lib, x, pp)
         gp.replay()
-        proj_ms = _events_ms(gp.replay, 1, stream) / edge_iters
+        proj_ms = _events_ms(gp.replay, 1, stream, rounds=5) / edge_iters
         # the two phases IN the step sequence: the layer's ping-pong workspaces
         # alternating, events between the launches (the isolated timings above
         # run each phase back to back on its own, so their sum need not equal
@@ -330,7 +336,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
             for _ in range(3):
                 plan.run(lib, x, pp, bias, out, csr)
             edge_ms = _events_ms(lambda: plan.run(lib, x, pp, bias, out, csr), edge_iters,
-                                 stream)
+                                 stream, rounds=5)
     hf = w.heads * w.out_channels
     comp = edge_kernel_compulsory_bytes(n, n, e_prime, w.heads, w.out_channels, w.concat)
     alg = edge_kernel_bytes(n, e_prime, w.heads, w.out_channels, w.concat)
