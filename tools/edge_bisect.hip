@@ -39,7 +39,11 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int G = 8, U = 4, H = 8, F = 8, PW = 32;  // plane width (floats)
+#ifdef SHAPE_ARXIV  // ogbn-arxiv shape: row-major 256-B rows, ~8 in-edges per row
+constexpr int G = 16, U = 4, H = 8, F = 8, PW = 64, NP = 1, NROWS = 169343, DEG_TRIALS = 28;
+#else  // PPI shape: two 128-B column planes, ~28 in-edges per row
+constexpr int G = 8, U = 4, H = 8, F = 8, PW = 32, NP = 2, NROWS = 44906, DEG_TRIALS = 108;
+#endif
 constexpr float kLog2e = 1.4426950408889634f;
 
 __device__ __forceinline__ float pair_sum(float v) {  // sum over lanes l, l ^ 1
@@ -59,9 +63,9 @@ __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const
                                                const float* __restrict__ s_dst,
                                                float* __restrict__ out, const int* __restrict__ order) {
     const int lane = threadIdx.x & 63, c = lane & (G - 1), gbase = lane & ~(G - 1);
-    const int sl = blockIdx.x & 1;
-    const unsigned blk = blockIdx.x >> 1;
-    const unsigned nblk = gridDim.x >> 1;
+    const int sl = NP > 1 ? (int)(blockIdx.x & 1) : 0;
+    const unsigned blk = NP > 1 ? blockIdx.x >> 1 : blockIdx.x;
+    const unsigned nblk = NP > 1 ? gridDim.x >> 1 : gridDim.x;
     const int g_first = (int)((blk * 256u + threadIdx.x) / G);
     const int g_stride = PERSIST ? (int)(nblk * 256u / G) : n;
     const float* __restrict__ W = wh + sl * plane_stride + 4 * c;
@@ -208,11 +212,11 @@ __global__ __launch_bounds__(256) void k_probe(const int* __restrict__ sb, const
 }
 
 int main() {
-    const int n = 44906;
+    const int n = NROWS;
     std::mt19937 rng(5);
     std::vector<int> deg(n);
     long long E = 0;
-    std::binomial_distribution<int> bd(27 * 4, 0.25);  // ~27 in-edges + the self-loop
+    std::binomial_distribution<int> bd(DEG_TRIALS, 0.25);  // in-edges + the self-loop
     for (int i = 0; i < n; ++i) {
         deg[i] = 1 + bd(rng);
         E += deg[i];
@@ -275,11 +279,11 @@ int main() {
         for (auto& v : colu) v = ud(rng);
         CK(hipMemcpy(d_colu, colu.data(), E * 4, hipMemcpyHostToDevice));
     }
-    const int blocks = ((n * G + 255) / 256) * 2;
+    const int blocks = ((n * G + 255) / 256) * NP;
     std::vector<std::pair<const char*, std::function<void()>>> vars;
     auto lib_on = [&](const int* cp) {
         return [=]() {
-            const int rc = gat_edge_aggregate_seg(d_sb, d_se, 1, cp, d_order, 0, n, d_wh, PW, n, 2,
+            const int rc = gat_edge_aggregate_seg(d_sb, d_se, 1, cp, d_order, 0, n, d_wh, PW, n, NP,
                                                   d_a, d_c, d_sd, H, F, 1, 0.2f, nullptr, nullptr,
                                                   0, 0, d_bias, d_out, (int)(E / n), nullptr);
             if (rc != 0) {
@@ -325,8 +329,8 @@ int main() {
             t[k].push_back(ms * 1e3f / 20);
         }
     }
-    printf("{\n \"shape\": {\"n\": %d, \"E\": %lld, \"planes\": 2, \"G\": %d, \"U\": %d},\n",
-           n, E, G, U);
+    printf("{\n \"shape\": {\"n\": %d, \"E\": %lld, \"planes\": %d, \"G\": %d, \"U\": %d},\n",
+           n, E, NP, G, U);
     printf(" \"note\": \"median us of 11 interleaved rounds of 20 launches each\",\n");
     for (size_t k = 0; k < vars.size(); ++k) {
         std::sort(t[k].begin(), t[k].end());
