@@ -902,7 +902,7 @@ __global__ __launch_bounds__(64) void k_edge_merge(
 // The same merge with a hub's segments spread over a 256-thread workgroup
 // (the default since round 5).  k_edge_merge walks all of a hub's segments in
 // one lane per head / column, three dependent loops of one load each: at
-// power-law Reddit (13k hubs, up to 116 segments) its launch took 120 us, set
+// power-law Reddit (3.4k hubs, up to 116 segments) its launch took 120 us, set
 // by the longest hubs' load chains.  Here thread t takes segments
 // s0 + g, s0 + g + ng, ... (g = t / H or t / HF), and the per-group partial
 // maxima / sums are combined in LDS in group order: deterministic, the same
