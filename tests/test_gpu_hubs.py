@@ -63,7 +63,10 @@ def _hub_case(n, e_uniform, hubs, fin, H, F, concat, seed):
 
 
 @pytest.mark.parametrize("H,F,concat", [(8, 8, True), (8, 8, False), (4, 8, True),
-                                        (2, 16, True), (16, 4, False)])
+                                        (2, 16, True), (16, 4, False),
+                                        # head counts that do not divide the merge's 256
+                                        # threads (segment groups of 85 / 42 threads)
+                                        (3, 8, True), (6, 4, False)])
 @pytest.mark.parametrize("slices", ["1", None])
 @pytest.mark.parametrize("merge", [None, "0"])
 def test_split_hubs_match_oracle(H, F, concat, slices, merge, monkeypatch):
