@@ -707,7 +707,9 @@ class GraphAttentionLayer(torch.nn.Module):
                 plans.popitem(last=False)
         out = torch.empty(plan.n, plan.hf if self.concat else self.output_channels,
                           dtype=torch.float32, device=x.device)
-        return plan.run(_lib.load(), x, self.packed(), self.bias.detach(), out, csr)
+        # (the plan reads only the bias' device pointer: no detached view needed;
+        # this path runs without autograd)
+        return plan.run(_lib.load(), x, self.packed(), self.bias, out, csr)
 
     def extra_repr(self) -> str:
         return (f"{self.input_channels}, {self.output_channels}, num_heads={self.num_heads}, "
