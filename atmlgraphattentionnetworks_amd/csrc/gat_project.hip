@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void k_project(
                     for (int i = 0; i < 4; ++i) {
                         const int rr = row0 + (lane >> 4) * 4 + i;
                         if (rr >= n) continue;
-                        Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
+                        if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
                         s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
                     }
                 }
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void k_project(
                         for (int i = 0; i < 4; ++i) {
                             const int rr = row0 + (lane >> 4) * 4 + i;
                             if (rr >= n) continue;
-                            Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
+                            if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
                             s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
                         }
                     }
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void k_project(
                 v1 = fmaf(v, a1[h * F + f], v1);
                 v2 = fmaf(v, a2[h * F + f], v2);
             }
-            Ss[(size_t)rr * ld_s + h] = v1 + c1[h];
+            if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = v1 + c1[h];
             s_dst[(size_t)rr * H + h] = v2 + c2[h];
         }
     }

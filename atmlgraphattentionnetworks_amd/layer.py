@@ -322,7 +322,7 @@ class ForwardPlan:
 
     __slots__ = ("n", "fin", "heads", "f", "hf", "hfp", "concat", "slope", "slices", "split",
                  "ws", "p_wh", "p_ss", "p_sd", "dev", "hint", "khint", "sched", "_csr", "bound",
-                 "bufs", "cur", "pws")
+                 "bufs", "cur", "pws", "need_ss")
 
     def __init__(self, x: torch.Tensor, csr: CSRGraph, heads: int, f: int, concat: bool,
                  negative_slope: float, pingpong: bool = False):
@@ -361,6 +361,15 @@ class ForwardPlan:
         # alive (CSRGraph is a tuple, so the weak reference is to its rowptr)
         self._csr = weakref.ref(csr.rowptr)
         self.bound = None  # (pp, bias, lib, project call, edge call) for run()
+        # the s_src table: only the gathered-score edge kernels read it (score
+        # activations other than LeakyReLU in [0, 1], heads whose F/4 is not a
+        # power of two, or GAT_EDGE_SCORE=gather); the fused kernels recompute
+        # s_src from the Wh row they gather, so the projection skips it (arxiv:
+        # 5.4 MB of stores).  GAT_PROJ_SS=1 (A/B knob): always write it.
+        self.need_ss = (not fused_score_ok(heads, f, negative_slope)
+                        or tuning.get("GAT_EDGE_SCORE") == "gather"
+                        or tuning.get("GAT_EDGE_KERNEL") == "generic"
+                        or tuning.get("GAT_PROJ_SS") == "1")
 
     def built_for(self, csr) -> bool:
         """This plan was built for `csr` (and that graph is still alive)."""
@@ -405,7 +414,8 @@ class ForwardPlan:
         p_order = 0 if csr.order is None else csr.order.data_ptr()
         fargs = []
         for p_wh, p_ss, p_sd in self.bufs:  # one argument list per workspace
-            fargs.append((n, fin, *pw, heads, f, self.slices, p_wh, p_ss, p_sd, sc.b.data_ptr(),
+            fargs.append((n, fin, *pw, heads, f, self.slices, p_wh,
+                          p_ss if self.need_ss else 0, p_sd, sc.b.data_ptr(),
                           sc.e.data_ptr(), sc.col.data_ptr(), p_order, int(self.concat),
                           self.slope, bias.data_ptr()))
         return (pp, bias.data_ptr(), lib, lib.gat_layer_forward, fargs, self.slices > 1)
@@ -418,7 +428,7 @@ class ForwardPlan:
             ld = n if self.slices > 1 else self.hfp
             # the sliced edge kernel recomputes s_src from the gathered row:
             # no s_src table then (as gat_project_sliced below)
-            p_ss = self.p_ss if self.slices == 1 else 0
+            p_ss = self.p_ss if self.slices == 1 and self.need_ss else 0
             rc = lib.gat_project_ex(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                     pp.a_src.data_ptr(), pp.c_src.data_ptr(),
                                     pp.a_dst.data_ptr(), pp.c_dst.data_ptr(), heads, f,
@@ -442,7 +452,8 @@ class ForwardPlan:
             self.slices = 1  # nothing was launched: the row-major table instead
         rc = lib.gat_project(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                              pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                             pp.c_dst.data_ptr(), heads, f, self.p_wh, self.hfp, self.p_ss,
+                             pp.c_dst.data_ptr(), heads, f, self.p_wh, self.hfp,
+                             self.p_ss if self.need_ss else 0,
                              heads, self.p_sd, stream)
         if rc:
             _lib.check(rc, "gat_project")
@@ -479,7 +490,8 @@ class ForwardPlan:
             return out
         rc = lib.gat_edge_aggregate(
             csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, self.p_wh, self.hfp,
-            self.p_ss, heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
+            self.p_ss if self.need_ss else 0, heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+            self.p_sd, heads, f,
             int(self.concat), self.slope, bias.data_ptr(), out.data_ptr(), 0, self.khint, stream)
         if rc:
             _lib.check(rc, "gat_edge_aggregate")

@@ -41,6 +41,8 @@ VARIANTS = {
     "no_xproj": {"GAT_EDGE_XPROJ": "0"},
     # short-row col values one chunk ahead instead of 8 chunks per load
     "no_rowcol": {"GAT_EDGE_ROWCOL": "0"},
+    # the s_src table written although the fused edge kernels recompute it
+    "proj_ss": {"GAT_PROJ_SS": "1"},
     "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
     "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds", "GAT_EDGE_SCHED": "0"},
     # the CSR-order launch (short rows take the scheduled copy by default)
@@ -78,7 +80,7 @@ def variant(request, monkeypatch):
               "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
               "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
               "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_XPROJ",
-              "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL"):
+              "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL", "GAT_PROJ_SS"):
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
