@@ -82,7 +82,9 @@ int gat_table_layout(int heads, int f, int* ld, int* s_off);
  *                      reference's stack/transpose [N,H,F] view (GAT.py:49-50)
  *                      made contiguous; columns [heads*f, round_up(heads*f, 4))
  *                      zeroed; ld_wh % 4 == 0, ld_wh >= round_up(heads*f, 4)
- *   s_src  [n, ld_s]   Wh_h . a_src_h + c_src_h   (ld_s >= heads)
+ *   s_src  [n, ld_s]   Wh_h . a_src_h + c_src_h   (ld_s >= heads); may be NULL
+ *                      (not written): the fused-score edge kernels recompute
+ *                      it from the Wh rows they gather
  *   s_dst  [n, heads]  Wh_h . a_dst_h + c_dst_h
  * Non-finite inputs: a row of x holding +/-Inf or NaN affects that row only;
  * every output the fp32 reference makes non-finite is non-finite here too, but
@@ -180,7 +182,7 @@ int gat_project_chunked(const float* x, int n, int fin, const float* w, const fl
 /*
  * gat_project_ex (ABI 8): every projection layout in one entry point, with an
  * optional caller-owned workspace.  slices == 1: Wh row-major with ld_wh =
- * ld_wh_or_n_table (as gat_project; s_src [n, ld_s] may not be NULL).  slices
+ * ld_wh_or_n_table (as gat_project; s_src [n, ld_s] or NULL).  slices
  * > 1: planes of n_table = ld_wh_or_n_table rows (as gat_project_sliced; s_src
  * may be NULL), and with chunk_rows > 0 the row chunks of gat_project_chunked
  * (chunk_stride floats apart).  workspace (16-B aligned, workspace_bytes >=
@@ -268,7 +270,8 @@ int gat_edge_merge_ex(const int* hub_rows, const int* seg_ptr, const int* seg_sl
 
 /*
  * The eval forward in one call: gat_project (slices == 1: row-major Wh at
- * ld = round_up(heads*f, 4), s_src [n, heads]) or gat_project_sliced (slices > 1,
+ * ld = round_up(heads*f, 4), s_src [n, heads] if not NULL: the edge kernel
+ * recomputes it, so callers pass NULL) or gat_project_sliced (slices > 1,
  * n_table = n, s_src unused), then gat_edge_aggregate_seg over a scheduled CSR
  * copy (seg_by_pos = 1: position p covers col[seg_begin[p] .. seg_end[p]) of
  * target row_order[p]; rows 0 .. n).  Replaces GAT.py:37-67 + GAT.py:54 for a
