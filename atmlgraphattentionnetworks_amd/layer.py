@@ -646,19 +646,25 @@ class GraphAttentionLayer(torch.nn.Module):
         return self._packed
 
     def _packed_aliases(self, pp: PackedParams) -> bool:
-        """Head 0's six parameters still start the six packed buffers."""
+        """Head 0's six parameters still start the six packed buffers (their
+        pointers at binding time are pp.key[0], [H], [2H] ... [5H]: the packed
+        buffers' own pointers, read once instead of on every forward)."""
         mods = self._modules
         if not mods["ws"]._modules:
             return True
         p0 = mods["ws"]._modules["0"]._parameters
         p1 = mods["attentions1"]._modules["0"]._parameters
         p2 = mods["attentions2"]._modules["0"]._parameters
-        return (p0["weight"].data_ptr() == pp.w.data_ptr()
-                and p0["bias"].data_ptr() == pp.b.data_ptr()
-                and p1["weight"].data_ptr() == pp.a_src.data_ptr()
-                and p1["bias"].data_ptr() == pp.c_src.data_ptr()
-                and p2["weight"].data_ptr() == pp.a_dst.data_ptr()
-                and p2["bias"].data_ptr() == pp.c_dst.data_ptr())
+        k, h = pp.key, self.num_heads
+        if len(k) != 6 * h:  # (not a _bind_packed key: compare the buffers themselves)
+            k = [pp.w.data_ptr()] * h + [pp.b.data_ptr()] * h + [pp.a_src.data_ptr()] * h + \
+                [pp.c_src.data_ptr()] * h + [pp.a_dst.data_ptr()] * h + [pp.c_dst.data_ptr()] * h
+        return (p0["weight"].data_ptr() == k[0]
+                and p0["bias"].data_ptr() == k[h]
+                and p1["weight"].data_ptr() == k[2 * h]
+                and p1["bias"].data_ptr() == k[3 * h]
+                and p2["weight"].data_ptr() == k[4 * h]
+                and p2["bias"].data_ptr() == k[5 * h])
 
     def _apply(self, fn, recurse=True):
         # .to() / .cuda() / .float() replace each parameter's storage: re-pack
