@@ -185,6 +185,7 @@ def csc_workspace_size(nnz: int, num_nodes: int) -> int:
 
 
 @functools.lru_cache(maxsize=None)  # pure function of the shape
+@functools.lru_cache(maxsize=None)  # pure function of the shape
 def weight_grad_workspace_size(num_nodes: int, fin: int, hf: int) -> int:
     out = ctypes.c_size_t()
     check(load().gat_weight_grad_workspace_size(num_nodes, fin, hf, ctypes.byref(out)),

@@ -90,18 +90,16 @@ class GATFunction(torch.autograd.Function):
         kink = act == _lib.GAT_ACT_LEAKY_RELU
         ws = torch.empty(n * (hfp + 3 * heads + hf + (hf + heads if kink else 0)),
                          dtype=torch.float32, device=dev)
-        wh = ws[:n * hfp].view(n, hfp)
-        o = n * hfp
-        s_src = ws[o:o + n * heads].view(n, heads)
-        s_dst = ws[o + n * heads:o + 2 * n * heads].view(n, heads)
-        lse = ws[o + 2 * n * heads:o + 3 * n * heads].view(n, heads)
-        y = ws[o + 3 * n * heads:o + 3 * n * heads + n * hf].view(n, hf)
+        # raw pointers into it (no per-call slice views: host cost of small graphs)
+        p_wh = ws.data_ptr()
+        p_ss = p_wh + 4 * n * hfp
+        p_sd, p_lse, p_y = p_ss + 4 * n * heads, p_ss + 8 * n * heads, p_ss + 12 * n * heads
         from .layer import project_workspace
         pws = project_workspace(dev, fin, heads, f)
         rc = lib.gat_project_ex(x.data_ptr(), n, fin, pp.w.data_ptr(), pp.b.data_ptr(),
                                 pp.a_src.data_ptr(), pp.c_src.data_ptr(), pp.a_dst.data_ptr(),
-                                pp.c_dst.data_ptr(), heads, f, 1, wh.data_ptr(), hfp,
-                                s_src.data_ptr(), heads, s_dst.data_ptr(), 0, 0,
+                                pp.c_dst.data_ptr(), heads, f, 1, p_wh, hfp,
+                                p_ss, heads, p_sd, 0, 0,
                                 0 if pws is None else pws.data_ptr(),
                                 0 if pws is None else pws.numel(), stream)
         if rc:
@@ -109,12 +107,12 @@ class GATFunction(torch.autograd.Function):
         out = torch.empty(n, hf if concat else f, dtype=torch.float32, device=dev)
         order = csr.order
         if kink:
-            p_q = y.data_ptr() + 4 * n * hf
+            p_q = p_y + 4 * n * hf
             rc = lib.gat_edge_aggregate_train(
                 csr.rowptr.data_ptr(), csr.col.data_ptr(), 0 if order is None else order.data_ptr(),
-                0, n, wh.data_ptr(), hfp, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
-                s_dst.data_ptr(), heads, f, int(concat), act_param, p, seed, p_seed,
-                bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(), p_q,
+                0, n, p_wh, hfp, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+                p_sd, heads, f, int(concat), act_param, p, seed, p_seed,
+                bias.data_ptr(), out.data_ptr(), p_lse, p_y, p_q,
                 p_q + 4 * n * hf, csr.kernel_hint(), stream)
             if rc and rc != _lib.GAT_EUNSUPPORTED:
                 _lib.check(rc, "gat_edge_aggregate_train")
@@ -122,10 +120,10 @@ class GATFunction(torch.autograd.Function):
         if not kink:
             rc = lib.gat_edge_aggregate_ex(
                 csr.rowptr.data_ptr(), csr.col.data_ptr(),
-                0 if order is None else order.data_ptr(), 0, n, wh.data_ptr(), hfp,
-                s_src.data_ptr(), heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
-                s_dst.data_ptr(), heads, f, int(concat), act, act_param, p, seed, p_seed,
-                bias.data_ptr(), out.data_ptr(), lse.data_ptr(), y.data_ptr(),
+                0 if order is None else order.data_ptr(), 0, n, p_wh, hfp,
+                p_ss, heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
+                p_sd, heads, f, int(concat), act, act_param, p, seed, p_seed,
+                bias.data_ptr(), out.data_ptr(), p_lse, p_y,
                 csr.kernel_hint(), stream)
             if rc:
                 _lib.check(rc, "gat_edge_aggregate_ex")
@@ -191,6 +189,15 @@ def _seed_ptr(ctx) -> int:
     return 0 if ctx.seed_slot is None else ctx.seed_slot.data_ptr()
 
 
+def _sums_tensor(pw: int, device) -> torch.Tensor:
+    """The per-parameter gradient sums get their own small allocation: the
+    bias / attention gradients handed to autograd are views of it, and views
+    of the backward workspace would keep that workspace (per-edge
+    coefficients on the stored path: 8 B per edge and head) alive for as long
+    as the gradients are."""
+    return torch.empty(pw, dtype=torch.float32, device=device)
+
+
 def _saved_layout(ctx, ws):
     """Pointers into the forward workspace: Wh | s_src | s_dst | lse | y."""
     heads, f = ctx.cfg[0], ctx.cfg[1]
@@ -252,11 +259,12 @@ def _backward_recompute(ctx, g, ws, csc, stream):
         base + 4 * o_dwh, hf, base + 4 * o_part, parts, hint, stream)
     if rc:
         _lib.check(rc, "gat_bwd_sources")
-    rc = lib.gat_sum_partials(base + 4 * o_part, parts, pw, base + 4 * o_ps,
+    ps = _sums_tensor(pw, g.device)
+    rc = lib.gat_sum_partials(base + 4 * o_part, parts, pw, ps.data_ptr(),
                               base + 4 * (o_ps + pw), 4 * sws, stream)
     if rc:
         _lib.check(rc, "gat_sum_partials")
-    return bw[o_dwh:o_part].view(n, hf), bw[o_ps:o_ps + pw]
+    return bw[o_dwh:o_part].view(n, hf), ps
 
 
 def _backward_stored(ctx, g, ws, csc, stream):
@@ -296,11 +304,12 @@ def _backward_stored(ctx, g, ws, csc, stream):
         bw.data_ptr() + 4 * o_dwh, hf, 0, p_part, parts, stream)
     if rc:
         _lib.check(rc, "gat_src_backward")
-    rc = lib.gat_sum_partials(p_part, parts, pw, bw.data_ptr() + 4 * o_ps,
+    ps = _sums_tensor(pw, g.device)
+    rc = lib.gat_sum_partials(p_part, parts, pw, ps.data_ptr(),
                               bw.data_ptr() + 4 * (o_ps + pw), 4 * sws, stream)
     if rc:
         _lib.check(rc, "gat_sum_partials")
-    return bw[o_dwh:o_part].view(n, hf), bw[o_ps:o_ps + pw]
+    return bw[o_dwh:o_part].view(n, hf), ps
 
 
 def gat_train_forward(layer, x: torch.Tensor, csr: CSRGraph, p: float, seed: int,

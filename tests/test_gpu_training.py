@@ -235,6 +235,25 @@ def test_train_forward_without_dropout_equals_eval_forward(monkeypatch):
     assert torch.allclose(out.detach(), ref, atol=1e-6, rtol=0)
 
 
+@pytest.mark.parametrize("kernel", ["default", "stored"])
+def test_param_grads_do_not_hold_the_backward_workspace(kernel, monkeypatch):
+    """The bias / attention gradients are views of a pw-float sums buffer of
+    their own, not of the backward workspace (which on the stored path holds
+    8 B per edge and head); the weight gradient is its own [H*F, Fin] buffer."""
+    if kernel != "default":
+        monkeypatch.setenv("GAT_BWD_KERNEL", kernel)
+    n, e, fin, H, F, concat = CASES[0]
+    layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat)
+    xd, out = _run(layer, x, ei)
+    out.sum().backward()
+    hf = H * F
+    pw = 3 * hf + 2 * H + hf
+    for name, p in layer.named_parameters():
+        nbytes = p.grad.untyped_storage().nbytes()
+        limit = 4 * hf * fin if name.startswith("ws.") and name.endswith("weight") else 4 * pw
+        assert nbytes <= limit, (name, nbytes, limit)
+
+
 def test_backward_is_deterministic():
     n, e, fin, H, F, concat = CASES[0]
     layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat)
