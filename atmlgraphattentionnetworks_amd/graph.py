@@ -154,7 +154,12 @@ def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
         return None
     seg = seg_len or hub_segment_len(num_edges)
     deg = (rowptr[1:] - rowptr[:-1]).to(torch.int64)
-    n_hub = int((deg > 2 * seg).sum())
+    # A/B knobs: GAT_HUB_MIN (split rows past this many edges, >= seg; default
+    # 2 * seg) and GAT_HUB_BAL=1 (a hub's segments of equal length, not seg
+    # edges and a short tail)
+    hub_min = tuning.get("GAT_HUB_MIN")
+    thresh = 2 * seg if hub_min is None else max(seg, int(hub_min))
+    n_hub = int((deg > thresh).sum())
     if n_hub == 0:
         return None
     o = order.to(torch.int64)
@@ -167,8 +172,10 @@ def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
     vhub = torch.repeat_interleave(torch.arange(n_hub, device=rowptr.device), nseg)
     k = torch.arange(n_v, device=rowptr.device) - vptr[vhub]
     rp = rowptr.to(torch.int64)
-    vb = rp[hub_rows][vhub] + k * seg
-    ve = torch.minimum(vb + seg, rp[hub_rows + 1][vhub])
+    slen = (hdeg + nseg - 1) // nseg if tuning.get("GAT_HUB_BAL") == "1" \
+        else torch.full_like(hdeg, seg)
+    vb = rp[hub_rows][vhub] + k * slen[vhub]
+    ve = torch.minimum(vb + slen[vhub], rp[hub_rows + 1][vhub])
     rest = o[n_hub:]
     i32 = torch.int32
     vrow = hub_rows[vhub]

@@ -14,7 +14,8 @@ from typing import Dict, Optional
 
 # knobs read on the Python side of the boundary
 PY_KNOBS = ("GAT_WH_SLICES", "GAT_EDGE_ORDER", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_SCHED",
-            "GAT_HUB_ORDER", "GAT_EDGE_SCORE", "GAT_EDGE_KERNEL", "GAT_PROJ_SS")
+            "GAT_HUB_ORDER", "GAT_EDGE_SCORE", "GAT_EDGE_KERNEL", "GAT_PROJ_SS",
+            "GAT_HUB_MIN", "GAT_HUB_BAL")
 
 _values: Dict[str, Optional[str]] = {}
 # bumped by every reload(): cached launch plans (layer.ForwardPlan) key on it,

@@ -31,7 +31,8 @@ KNOBS = ("GAT_EDGE_R", "GAT_EDGE_U", "GAT_EDGE_V", "GAT_EDGE_PIPE", "GAT_EDGE_LD
          "GAT_PROJ_WRES", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WRES_NW", "GAT_STORE_WT",
          "GAT_EDGE_SCHED", "GAT_EDGE_SPLIT", "GAT_EDGE_LDSDMA", "GAT_PROJ_WG", "GAT_PROJ_X3V",
          "GAT_HUB_ORDER", "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT",
-         "GAT_EDGE_XPROJ", "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL", "GAT_PROJ_SS", "GAT_EDGE_SCORE")
+         "GAT_EDGE_XPROJ", "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL", "GAT_PROJ_SS", "GAT_EDGE_SCORE",
+         "GAT_HUB_MIN", "GAT_HUB_BAL")
 
 
 def parse(spec):
