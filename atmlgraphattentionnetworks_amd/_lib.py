@@ -18,7 +18,7 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 10
+GAT_ABI_VERSION = 11
 GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
 GAT_SEG_LOAD = 1
 GAT_SEG_STORE = 2
@@ -103,6 +103,7 @@ SIGNATURES = {
                                    _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                                    _c_vp, _c_vp, _c_vp, _c_int, _c_float, _c_vp, _c_vp, _c_int,
                                    _c_vp]),
+    "gat_layer_forward_fuses": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_float]),
     "gat_input_grad": (_c_int, [_c_vp, _c_int, _c_int, _c_int, _c_vp, _c_int, _c_vp, _c_int,
                                 _c_vp]),
     "gat_sum_partials_workspace_size": (_c_int, [_c_int, _c_ll, _c_size_p]),
@@ -184,7 +185,6 @@ def csc_workspace_size(nnz: int, num_nodes: int) -> int:
     return out.value
 
 
-@functools.lru_cache(maxsize=None)  # pure function of the shape
 @functools.lru_cache(maxsize=None)  # pure function of the shape
 def weight_grad_workspace_size(num_nodes: int, fin: int, hf: int) -> int:
     out = ctypes.c_size_t()

@@ -83,6 +83,9 @@ def _roofline(r: Dict) -> Dict:
             "algorithmic_bytes_per_launch": r.get("algorithmic_bytes_per_launch"),
             "algorithmic_model": "compulsory bytes: col 4/edge, rowptr+schedule 8/row, Wh table "
                                  "once, s_dst 4H/row, output 4C/row (DESIGN.md §5)",
+            "frac_8d": r.get("frac_8d"), "achieved_8d": r.get("achieved_8d"),
+            "model_8d": "SURVEY.md §8(d): (4 + 4HF + 4H) B/edge + (4 + 4H + 4C) B/row, every "
+                        "gather as if from HBM (> 1: rows re-read from L2 / Infinity Cache)",
             "traffic_x_algorithmic": fab.get("x_compulsory"), "l2_hit": fab.get("l2_hit_rate"),
             "l2_gather_ceiling_frac": l2.get("frac_of_gather_ceiling")}
 

@@ -1,22 +1,28 @@
-// MI355X GAT library: ABI version, table layout and the A/B knob snapshot.
+// MI355X GAT library: ABI version, table layout and the knob snapshot.
 
 #include "gat_common.h"
 
 namespace gat_detail __attribute__((visibility("hidden"))) {
 
-// Kernel-choice knobs for A/B measurement (tools/, tests; not part of the
-// ABI).  The environment is read ONCE, at the first launch, into a snapshot;
-// gat_tuning_reload() re-reads it (for the tools and tests that switch
-// variants within one process).  The specialised kernels are the default
-// wherever the shape allows them.
+// Kernel-choice knobs (not part of the ABI): each forces one of two product
+// paths that a shape or a graph can also reach, so that the tests can compare
+// them on one input (bitwise where the arithmetic is the same).  The
+// environment is read ONCE, at the first launch, into a snapshot;
+// gat_tuning_reload() re-reads it (for the tests that switch paths within one
+// process).  The defaults are the measured-fastest choices; the round-1..5
+// A/B knobs whose losing arms are recorded under profiles/ were removed with
+// their kernels in round 6.
 static const char* const kKnobNames[] = {
-    "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_EDGE_LDS",  "GAT_EDGE_V",   "GAT_EDGE_U",
-    "GAT_EDGE_PIPE",   "GAT_EDGE_SCORE",  "GAT_EDGE_KERNEL", "GAT_BWD_LDS", "GAT_BWD_U",
-    "GAT_BWD_KERNEL",  "GAT_BWD_WAVES",   "GAT_HUB_SEG",     "GAT_PROJ_X3",
-    "GAT_PROJ_BM",     "GAT_PROJ_WRES",   "GAT_PROJ_WRES_WGS", "GAT_BWD_KINK",
-    "GAT_WGRAD_LW",    "GAT_STORE_WT",    "GAT_PROJ_WK_DIRECT", "GAT_EDGE_SPLIT",
-    "GAT_PROJ_X3V",    "GAT_PROJ_WG",     "GAT_EDGE_LDSDMA", "GAT_PROJ_PRESPLIT", "GAT_BWD_SL",
-    "GAT_EDGE_HL",     "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_XPROJ", "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL"};
+    "GAT_EDGE_U",      // edges per chunk: 4, 8 or 16 (default by edges per row)
+    "GAT_EDGE_V",      // float4s per lane: 1 or 2 (default by edges per row)
+    "GAT_EDGE_PIPE",   // 0: the U = 16, V = 2 kernel without gathers one chunk ahead
+    "GAT_EDGE_SPLIT",  // lane groups per row: 1, 2 or 4 (default by launch size)
+    "GAT_EDGE_ROWCOL", // 0: short-row col values one chunk ahead, not 8 per load
+    "GAT_EDGE_XPROJ",  // 0: Fin <= 4 as projection + edge kernel, not fused
+    "GAT_BWD_KINK",    // 0: the backward's target pass over the edges, not the kink sums
+    "GAT_BWD_SL",      // 0: the generic source pass, not the straight-line HF = 64 one
+    "GAT_BWD_KERNEL",  // stored | generic: the stored-coefficient backward
+};
 constexpr int kNumKnobs = (int)(sizeof(kKnobNames) / sizeof(kKnobNames[0]));
 
 struct KnobSnapshot {
@@ -44,11 +50,6 @@ const char* knob(const char* name) {
     for (int i = 0; i < kNumKnobs; ++i)
         if (std::strcmp(kKnobNames[i], name) == 0) return g_knobs.set[i] ? g_knobs.val[i] : nullptr;
     return nullptr;
-}
-
-int store_wt_on() {
-    const char* v = knob("GAT_STORE_WT");
-    return v != nullptr ? std::max(0, std::min(3, std::atoi(v))) : 1;
 }
 
 bool kernel_choice(const char* env, const char* slow) {

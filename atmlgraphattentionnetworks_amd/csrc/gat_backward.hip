@@ -1012,23 +1012,10 @@ int gat_bwd_table_layout(int heads, int f, int concat, int* ld_t) {
     return GAT_OK;
 }
 
-// edges per chunk of the recompute backward kernels: the forward's thresholds;
-// GAT_BWD_U overrides (A/B knob)
-// GAT_BWD_LDS (A/B knob): dynamic LDS bytes per block for the recompute
-// backward kernels, unused by them — caps the blocks resident per CU
-static size_t bwd_lds_bytes() {
-    const char* v = knob("GAT_BWD_LDS");
-    return v != nullptr ? (size_t)std::atol(v) : 0;
-}
-
+// edges per chunk of the recompute backward kernels: the forward's thresholds
 static int bwd_unroll(int hint) {
     hint &= ~GAT_HINT_LOCAL;
-    int u = hint <= 0 ? 8 : hint <= 32 ? 4 : hint <= 64 ? 8 : 16;
-    if (const char* v = knob("GAT_BWD_U")) {
-        const int x = std::atoi(v);
-        u = (x == 4 || x == 16) ? x : 8;
-    }
-    return u;
+    return hint <= 0 ? 8 : hint <= 32 ? 4 : hint <= 64 ? 8 : 16;
 }
 
 static bool bwd_recompute_ok(int heads, int f, float slope, const float* wh, int ld_wh) {
@@ -1063,17 +1050,17 @@ int gat_bwd_targets(const int* rowptr, const int* col, const int* row_order, int
     int u = bwd_unroll(edges_per_row_hint);
     const long long threads = (long long)rows * g;
     const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
-    const size_t bwd_lds = bwd_lds_bytes();
-#define GAT_BT(G, UU)                                                                         \
-    hipLaunchKernelGGL((k_bwd_targets<G, UU>), grid, block, bwd_lds, st, rowptr, col, row_order,    \
+    #define GAT_BT(G, UU)                                                                         \
+    hipLaunchKernelGGL((k_bwd_targets<G, UU>), grid, block, 0, st, rowptr, col, row_order,    \
                        row_begin, row_end, wh, ld_wh, a_src, c_src, s_dst, lse, y_heads,      \
                        grad_out, heads, f, hf, concat, negative_slope, drop, ds_dst, table,   \
                        ld_t)
+    // (the kink-sum table, gat_bwd_table, is the default where the forward can
+    // form the sums: this pass serves the other head widths, at U = 8)
+    (void)u;
 #define GAT_BT_U(G)                      \
     case G:                              \
-        if (u == 4) { GAT_BT(G, 4); }    \
-        else if (u == 16) { GAT_BT(G, 16); } \
-        else { GAT_BT(G, 8); }           \
+        GAT_BT(G, 8);                    \
         break;
     switch (g) {
         GAT_BT_U(1) GAT_BT_U(2) GAT_BT_U(4) GAT_BT_U(8) GAT_BT_U(16) GAT_BT_U(32) GAT_BT_U(64)
@@ -1116,8 +1103,7 @@ int gat_bwd_sources_parts(int num_nodes, int heads, int f, int* num_parts) {
     if (num_nodes < 0 || heads <= 0 || f <= 0 || num_parts == nullptr) return GAT_EINVAL;
     const int g = next_pow2((heads * f + 3) / 4);
     const long long waves = ((long long)num_nodes * g + kWave - 1) / kWave;
-    long long cap = 65536;  // GAT_BWD_WAVES overrides (A/B knob)
-    if (const char* v = knob("GAT_BWD_WAVES")) cap = std::atoll(v) > 0 ? std::atoll(v) : cap;
+    const long long cap = 65536;
     long long w = waves < cap ? waves : cap;
     w = (w + 3) / 4 * 4;  // whole 256-thread blocks
     *num_parts = (int)(w < 4 ? 4 : w);
@@ -1143,16 +1129,21 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
     const int g = next_pow2(hf / 4);
     int u = bwd_unroll(edges_per_row_hint);
     const dim3 grid(num_parts / 4), block(256);
-    const size_t bwd_lds = bwd_lds_bytes();
-#define GAT_BS(G, UU)                                                                         \
-    hipLaunchKernelGGL((k_bwd_sources<G, UU>), grid, block, bwd_lds, st, csc_ptr, csc_dst, csc_eid,  \
+    #define GAT_BS(G, UU)                                                                         \
+    hipLaunchKernelGGL((k_bwd_sources<G, UU>), grid, block, 0, st, csc_ptr, csc_dst, csc_eid,  \
                        num_nodes, wh, ld_wh, table, ld_t, ds_dst, a_src, c_src, a_dst, heads, \
                        f, hf, concat, negative_slope, drop, dwh, ld_dwh, partials)
-#define GAT_BS_U(G)                      \
-    case G:                              \
-        if (u == 4) { GAT_BS(G, 4); }    \
-        else if (u == 16) { GAT_BS(G, 16); } \
-        else { GAT_BS(G, 8); }           \
+    // every chunk length for the HF = 32 / 64 lane groups (G = 8, 16); U = 8
+    // for the other widths
+#define GAT_BS_U(G)                                      \
+    case G:                                              \
+        if constexpr (G == 8 || G == 16) {               \
+            if (u == 4) { GAT_BS(G, 4); }                \
+            else if (u == 16) { GAT_BS(G, 16); }         \
+            else { GAT_BS(G, 8); }                       \
+        } else {                                         \
+            GAT_BS(G, 8);                                \
+        }                                                \
         break;
     // the straight-line kernel for HF = 64 (the default; GAT_BWD_SL=0 is the A/B
     // knob back to k_bwd_sources): Reddit training step 8.79 -> 8.55 ms, PPI
@@ -1170,7 +1161,7 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
     if (sl) {
         const bool dr = drop.thresh != 0u;
 #define GAT_BSL(UU, HLV, DR)                                                                   \
-    hipLaunchKernelGGL((k_bwd_sources_sl<UU, HLV, DR>), grid, block, bwd_lds, st, csc_ptr, csc_dst, \
+    hipLaunchKernelGGL((k_bwd_sources_sl<UU, HLV, DR>), grid, block, 0, st, csc_ptr, csc_dst, \
                        csc_eid, num_nodes, wh, ld_wh, table, ld_t, ds_dst, a_src, c_src, a_dst,   \
                        heads, f, hf, concat, negative_slope, drop, dwh, ld_dwh, partials)
 #define GAT_BSL_HL(UU, HLV) \
@@ -1229,10 +1220,10 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
     hipLaunchKernelGGL((k_edge_bwd_grp<G, UU>), grid, block, 0, st, rowptr, col, row_order,   \
                        row_begin, row_end, csr_to_csc, wh, ld_wh, a_src, c_src, s_dst, lse,   \
                        y_heads, grad_out, heads, f, hf, concat, act_param, drop, ds_dst, az)
+        (void)u;  // (the knob-only stored path for LeakyReLU: U = 8)
 #define GAT_BWD_GRP_U(G)                       \
     case G:                                    \
-        if (u == 4) { GAT_BWD_GRP(G, 4); }     \
-        else { GAT_BWD_GRP(G, 8); }            \
+        GAT_BWD_GRP(G, 8);                     \
         break;
         switch (g) {
             GAT_BWD_GRP_U(1) GAT_BWD_GRP_U(2) GAT_BWD_GRP_U(4) GAT_BWD_GRP_U(8)
@@ -1321,10 +1312,8 @@ int gat_weight_grad(const float* x, int num_nodes, int fin, const float* dwh, in
     float* part = (float*)workspace;
     const dim3 grid((fin + 63) / 64, chunks, (hf + 63) / 64), block(256);
     // x rows read LW floats at a time where fin and x's alignment allow
-    // (GAT_WGRAD_LW A/B knob caps it)
     const uintptr_t xa = reinterpret_cast<uintptr_t>(x);
-    int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
-    if (const char* v = knob("GAT_WGRAD_LW")) lw = std::min(lw, std::max(1, std::atoi(v)));
+    const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
     if (lw == 4)
         hipLaunchKernelGGL(k_wgrad<4>, grid, block, 0, st, dwh, ld_dwh, x, num_nodes, fin, hf,
                            rows, part);

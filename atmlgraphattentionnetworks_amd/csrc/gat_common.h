@@ -2,7 +2,7 @@
 // MI355X (gfx950) GAT attention layer: HIP kernels + C-ABI — shared helpers.
 //
 // The library is five translation units that include this header:
-//   gat_abi.hip       ABI version, table layout, the A/B knob snapshot
+//   gat_abi.hip       ABI version, table layout, the knob snapshot
 //   gat_project.hip   projection + score epilogue (gat_project*)
 //   gat_edge.hip      fused edge kernel, hub merge, gat_layer_forward
 //   gat_csr.hip       CSR / CSC builds (gat_csr_build, gat_csc_build)
@@ -48,13 +48,11 @@
 
 #include "../../include/gat_amd.h"
 
-// Kernel-choice knobs for A/B measurement (tools/, tests; not part of the
-// ABI), snapshotted from the environment at the first launch (gat_abi.hip).
+// Kernel-choice knobs (tests and A/B measurement; not part of the ABI),
+// snapshotted from the environment at the first launch (gat_abi.hip).
 namespace gat_detail __attribute__((visibility("hidden"))) {
 const char* knob(const char* name);
 void snapshot_knobs();
-// GAT_STORE_WT (A/B knob): 1 = final outputs stored write-through (sc1), 0 = plain
-int store_wt_on();
 bool kernel_choice(const char* env, const char* slow);
 }  // namespace gat_detail
 using namespace gat_detail;
@@ -232,19 +230,13 @@ __device__ __forceinline__ f32x4 fma4(float s, f32x4 v, f32x4 acc) {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr size_t kWtMaxOff = 0x7FFFFFF0u;
 
-// wt: 0 plain store; 1 write-through (sc1, the default); 2 non-temporal (nt,
-// streamed past the caches); 3 nt + sc1 (GAT_STORE_WT A/B knob values)
+// wt: 0 plain store; 1 write-through (sc1; the final outputs).  (Round 3
+// measured plain, sc0, sc1, nt and nt + sc1 stores; sc1 won: DESIGN.md §3.1.)
 __device__ __forceinline__ void store_out4(float* base, size_t idx, f32x4 v, int wt) {
     const size_t off = idx * sizeof(float);
     if (wt && off < kWtMaxOff) {
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
-        const u32x4 bits = __builtin_bit_cast(u32x4, v);
-        if (wt == 2)
-            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (int)off, 0, 2);
-        else if (wt == 3)
-            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (int)off, 0, 18);
-        else
-            __builtin_amdgcn_raw_buffer_store_b128(bits, rsrc, (int)off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc, (int)off, 0, 16);
     } else {
         *reinterpret_cast<f32x4*>(base + idx) = v;
     }
@@ -254,12 +246,7 @@ __device__ __forceinline__ void store_out1(float* base, size_t idx, float v, int
     const size_t off = idx * sizeof(float);
     if (wt && off < kWtMaxOff) {
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
-        if (wt == 2)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 2);
-        else if (wt == 3)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 18);
-        else
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc, (int)off, 0, 16);
     } else {
         base[idx] = v;
     }

@@ -56,13 +56,26 @@ __global__ void k_csr_col(const unsigned long long* __restrict__ sorted_keys, lo
         col[k] = (int)(sorted_keys[k] & mask);
 }
 
-__global__ void k_degree_keys(const int* __restrict__ rowptr, int n, unsigned* __restrict__ keys,
-                              int* __restrict__ rows) {
+// rows by descending in-degree, ties by ascending row id (the order of a
+// stable descending sort): one 64-bit key ((2^kd - 1 - degree) << kb | row),
+// sorted ascending by the same u64 radix sort as the CSR keys (one sort
+// instantiation in the library instead of three)
+__global__ void k_degree_keys(const int* __restrict__ rowptr, int n, unsigned kb, unsigned kd,
+                              unsigned long long* __restrict__ keys) {
     const long long stride = (long long)gridDim.x * blockDim.x;
+    const unsigned long long top = (1ull << kd) - 1ull;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
-        keys[i] = (unsigned)(rowptr[i + 1] - rowptr[i]);
-        rows[i] = (int)i;
+        const unsigned long long deg = (unsigned long long)(rowptr[i + 1] - rowptr[i]);
+        keys[i] = ((top - deg) << kb) | (unsigned long long)i;
     }
+}
+
+__global__ void k_low_bits(const unsigned long long* __restrict__ keys, long long n, unsigned kb,
+                           int* __restrict__ out) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    const unsigned long long mask = (1ull << kb) - 1ull;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = (int)(keys[i] & mask);
 }
 
 // ---------------------------------------------------------------------------
@@ -72,38 +85,39 @@ __global__ void k_degree_keys(const int* __restrict__ rowptr, int n, unsigned* _
 //   csc_dst[c]       target row of the edge in CSC slot c
 //   csc_eid[c]       CSR position of the edge in CSC slot c
 //   csr_to_csc[k]    CSC slot of CSR position k
-// Built by a stable radix sort of (col[k], k): within a source, edges keep
-// CSR order, so every reduction over them is deterministic.  The target row
-// of a CSR position is found by binary search in rowptr (L2-resident) rather
-// than gathered from a per-edge array.
+// Built by one radix sort of 64-bit keys (col[k] << kn | k), k < 2^kn: within
+// a source, edges keep CSR order, so every reduction over them is
+// deterministic.  The target row of a CSR position is found by binary search
+// in rowptr (L2-resident) rather than gathered from a per-edge array.
 // ---------------------------------------------------------------------------
-__global__ void k_csc_keys(long long nnz, const int* __restrict__ col,
-                           unsigned* __restrict__ keys, int* __restrict__ vals) {
+__global__ void k_csc_keys(long long nnz, const int* __restrict__ col, unsigned kn,
+                           unsigned long long* __restrict__ keys) {
     const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < nnz; k += stride) {
-        keys[k] = (unsigned)col[k];
-        vals[k] = (int)k;
-    }
+    for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < nnz; k += stride)
+        keys[k] = ((unsigned long long)(unsigned)col[k] << kn) | (unsigned long long)k;
 }
 
-__global__ void k_csc_ptr(const unsigned* __restrict__ sorted_keys, long long nnz, int n,
-                          int* __restrict__ csc_ptr) {
+__global__ void k_csc_ptr(const unsigned long long* __restrict__ sorted_keys, long long nnz,
+                          int n, unsigned kn, int* __restrict__ csc_ptr) {
     const long long j = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     if (j > n) return;
     long long lo = 0, hi = nnz;
     while (lo < hi) {
         const long long mid = (lo + hi) >> 1;
-        if (sorted_keys[mid] < (unsigned)j) lo = mid + 1; else hi = mid;
+        if ((long long)(sorted_keys[mid] >> kn) < j) lo = mid + 1; else hi = mid;
     }
     csc_ptr[j] = (int)lo;
 }
 
-__global__ void k_csc_fill(const int* __restrict__ sorted_vals, const int* __restrict__ rowptr,
-                           int n, long long nnz, int* __restrict__ csc_dst,
+__global__ void k_csc_fill(const unsigned long long* __restrict__ sorted_keys, unsigned kn,
+                           const int* __restrict__ rowptr, int n, long long nnz,
+                           int* __restrict__ csc_eid, int* __restrict__ csc_dst,
                            int* __restrict__ csr_to_csc) {
     const long long stride = (long long)gridDim.x * blockDim.x;
+    const unsigned long long mask = (1ull << kn) - 1ull;
     for (long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x; c < nnz; c += stride) {
-        const int k = sorted_vals[c];
+        const int k = (int)(sorted_keys[c] & mask);
+        if (csc_eid != nullptr) csc_eid[c] = k;
         // the row holding CSR position k: last i with rowptr[i] <= k
         int lo = 0, hi = n - 1;
         while (lo < hi) {
@@ -115,26 +129,20 @@ __global__ void k_csc_fill(const int* __restrict__ sorted_vals, const int* __res
     }
 }
 
-unsigned key_bits(int n) {
+// bits to hold values in [0, n)
+unsigned key_bits(long long n) {
     unsigned b = 1;
-    while (b < 31 && (1u << b) < (unsigned)n) ++b;
+    while (b < 40 && (1ll << b) < n) ++b;
     return b;
 }
 
-size_t radix_tmp_bytes(long long E, int n) {
+// temporary storage of the library's one radix sort (u64 keys) for `count`
+// keys of `bits` bits
+size_t key_sort_tmp_bytes(long long count, unsigned bits) {
     size_t tmp = 0;
-    unsigned* k = nullptr;
-    int* v = nullptr;
-    const hipError_t e = rocprim::radix_sort_pairs(nullptr, tmp, k, k, v, v, (size_t)E, 0u, key_bits(n));
-    return e == hipSuccess ? tmp : 0;
-}
-
-size_t degree_sort_tmp_bytes(int n) {
-    size_t tmp = 0;
-    unsigned* k = nullptr;
-    int* v = nullptr;
-    const hipError_t e = rocprim::radix_sort_pairs_desc(nullptr, tmp, k, k, v, v,
-                                                        (size_t)(n > 0 ? n : 1), 0u, 32u);
+    unsigned long long* k = nullptr;
+    const hipError_t e = rocprim::radix_sort_keys(nullptr, tmp, k, k, (size_t)(count > 0 ? count : 1),
+                                                  0u, bits);
     return e == hipSuccess ? tmp : 0;
 }
 
@@ -142,25 +150,17 @@ size_t degree_sort_tmp_bytes(int n) {
 
 extern "C" {
 
-static size_t csr_key_sort_tmp_bytes(long long nnz, int n) {
-    size_t tmp = 0;
-    unsigned long long* k = nullptr;
-    const unsigned kb = key_bits(n);
-    const hipError_t e = rocprim::radix_sort_keys(nullptr, tmp, k, k, (size_t)nnz, 0u, 2 * kb);
-    return e == hipSuccess ? tmp : 0;
-}
-
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes) {
     if (num_edges < 0 || num_nodes < 0 || bytes == nullptr) return GAT_EINVAL;
     if (num_edges + num_nodes > 0x7fffffffLL) return GAT_EUNSUPPORTED;
     long long nnz = num_edges + num_nodes;
     if (nnz < 1) nnz = 1;
-    const size_t t1 = csr_key_sort_tmp_bytes(nnz, num_nodes > 0 ? num_nodes : 1);
-    const size_t t2 = degree_sort_tmp_bytes(num_nodes);
-    const size_t kb = align_up((size_t)nnz * 8);
-    const size_t nb = align_up((size_t)(num_nodes > 0 ? num_nodes : 1) * 4);
-    const size_t a = 2 * kb;                       // keys in / out
-    const size_t b = 4 * nb;                       // degree-sort buffers
+    const int n = num_nodes > 0 ? num_nodes : 1;
+    const unsigned kb = key_bits(n), kd = key_bits(nnz + 1);
+    const size_t t1 = key_sort_tmp_bytes(nnz, 2 * kb);
+    const size_t t2 = key_sort_tmp_bytes(n, kb + kd);
+    const size_t a = 2 * align_up((size_t)nnz * 8);  // keys in / out (edges)
+    const size_t b = 2 * align_up((size_t)n * 8);    // keys in / out (rows)
     *bytes = (a > b ? a : b) + align_up(t1 > t2 ? t1 : t2);
     return GAT_OK;
 }
@@ -185,10 +185,10 @@ int gat_csr_build(const long long* edge_index, long long num_edges, int num_node
         return status_of(hipMemsetAsync(rowptr, 0, sizeof(int), st));
     }
     const long long nnz = num_edges + num_nodes;
-    const unsigned kb = key_bits(num_nodes);
+    const unsigned kb = key_bits(num_nodes), kd = key_bits(nnz + 1);
     const size_t keyb = align_up((size_t)nnz * 8);
-    const size_t nb = align_up((size_t)num_nodes * 4);
-    const size_t region = 2 * keyb > 4 * nb ? 2 * keyb : 4 * nb;
+    const size_t nb = align_up((size_t)num_nodes * 8);
+    const size_t region = 2 * keyb > 2 * nb ? 2 * keyb : 2 * nb;
     char* ws = (char*)workspace;
     unsigned long long* keys_in = (unsigned long long*)ws;
     unsigned long long* keys_out = (unsigned long long*)(ws + keyb);
@@ -203,16 +203,17 @@ int gat_csr_build(const long long* edge_index, long long num_edges, int num_node
     hipLaunchKernelGGL(k_csr_col, dim3(grid_for(nnz, 256)), dim3(256), 0, st, keys_out, nnz, kb,
                        col);
     if (row_order != nullptr) {
-        // rows by descending in-degree (stable): the edge kernel's schedule
-        unsigned* dkeys_in = (unsigned*)ws;
-        int* dvals_in = (int*)(ws + nb);
-        unsigned* dkeys_out = (unsigned*)(ws + 2 * nb);
+        // rows by descending in-degree (ties by row id): the edge kernel's schedule
+        unsigned long long* dkeys_in = (unsigned long long*)ws;
+        unsigned long long* dkeys_out = (unsigned long long*)(ws + nb);
         hipLaunchKernelGGL(k_degree_keys, dim3(grid_for(num_nodes, 256)), dim3(256), 0, st,
-                           rowptr, num_nodes, dkeys_in, dvals_in);
+                           rowptr, num_nodes, kb, kd, dkeys_in);
         tmp_bytes = need - region;
-        e = rocprim::radix_sort_pairs_desc(tmp, tmp_bytes, dkeys_in, dkeys_out, dvals_in,
-                                           row_order, (size_t)num_nodes, 0u, 32u, st);
+        e = rocprim::radix_sort_keys(tmp, tmp_bytes, dkeys_in, dkeys_out, (size_t)num_nodes, 0u,
+                                     kb + kd, st);
         if (e != hipSuccess) return status_of(e);
+        hipLaunchKernelGGL(k_low_bits, dim3(grid_for(num_nodes, 256)), dim3(256), 0, st,
+                           dkeys_out, (long long)num_nodes, kb, row_order);
     }
     return status_of(hipGetLastError());
 }
@@ -220,8 +221,9 @@ int gat_csr_build(const long long* edge_index, long long num_edges, int num_node
 int gat_csc_workspace_size(long long nnz, int num_nodes, size_t* bytes) {
     if (nnz < 0 || num_nodes < 0 || bytes == nullptr) return GAT_EINVAL;
     if (nnz > 0x7fffffffLL) return GAT_EUNSUPPORTED;
-    const size_t eb = align_up((size_t)(nnz > 0 ? nnz : 1) * 4);
-    *bytes = 4 * eb + align_up(radix_tmp_bytes(nnz, num_nodes > 0 ? num_nodes : 1));
+    const size_t eb = align_up((size_t)(nnz > 0 ? nnz : 1) * 8);
+    const unsigned bits = key_bits(num_nodes > 0 ? num_nodes : 1) + key_bits(nnz > 0 ? nnz : 1);
+    *bytes = 2 * eb + align_up(key_sort_tmp_bytes(nnz, bits));
     return GAT_OK;
 }
 
@@ -236,23 +238,22 @@ int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nn
     hipStream_t st = (hipStream_t)stream;
     if (num_nodes == 0) return GAT_OK;
     if (nnz == 0) return status_of(hipMemsetAsync(csc_ptr, 0, sizeof(int) * (num_nodes + 1), st));
-    const size_t eb = align_up((size_t)nnz * 4);
+    const size_t eb = align_up((size_t)nnz * 8);
+    const unsigned kn = key_bits(nnz), bits = key_bits(num_nodes) + kn;
     char* ws = (char*)workspace;
-    unsigned* keys_in = (unsigned*)ws;
-    int* vals_in = (int*)(ws + eb);
-    unsigned* keys_out = (unsigned*)(ws + 2 * eb);
-    int* vals_out = csc_eid != nullptr ? csc_eid : (int*)(ws + 3 * eb);
-    void* tmp = ws + 4 * eb;
-    hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(nnz, 256)), dim3(256), 0, st, nnz, col, keys_in,
-                       vals_in);
-    size_t tmp_bytes = need - 4 * eb;
-    hipError_t e = rocprim::radix_sort_pairs(tmp, tmp_bytes, keys_in, keys_out, vals_in, vals_out,
-                                             (size_t)nnz, 0u, key_bits(num_nodes), st);
+    unsigned long long* keys_in = (unsigned long long*)ws;
+    unsigned long long* keys_out = (unsigned long long*)(ws + eb);
+    void* tmp = ws + 2 * eb;
+    hipLaunchKernelGGL(k_csc_keys, dim3(grid_for(nnz, 256)), dim3(256), 0, st, nnz, col, kn,
+                       keys_in);
+    size_t tmp_bytes = need - 2 * eb;
+    hipError_t e = rocprim::radix_sort_keys(tmp, tmp_bytes, keys_in, keys_out, (size_t)nnz, 0u,
+                                            bits, st);
     if (e != hipSuccess) return status_of(e);
     hipLaunchKernelGGL(k_csc_ptr, dim3((num_nodes + 1 + 255) / 256), dim3(256), 0, st, keys_out,
-                       nnz, num_nodes, csc_ptr);
-    hipLaunchKernelGGL(k_csc_fill, dim3(grid_for(nnz, 256)), dim3(256), 0, st, vals_out, rowptr,
-                       num_nodes, nnz, csc_dst, csr_to_csc);
+                       nnz, num_nodes, kn, csc_ptr);
+    hipLaunchKernelGGL(k_csc_fill, dim3(grid_for(nnz, 256)), dim3(256), 0, st, keys_out, kn,
+                       rowptr, num_nodes, nnz, csc_eid, csc_dst, csr_to_csc);
     return status_of(hipGetLastError());
 }
 

@@ -1,5 +1,5 @@
 // MI355X GAT edge kernel: segmented softmax + aggregation over the CSR by
-// target (GAT.py:53-67).  Kernels k_edge_fwd, k_edge_grp, k_edge_merge; C-ABI
+// target (GAT.py:53-67).  Kernels k_edge_fwd, k_edge_grp, k_edge_merge_wg; C-ABI
 // gat_edge_aggregate*, gat_edge_merge, gat_layer_forward.
 
 #include "gat_common.h"
@@ -22,7 +22,10 @@ namespace {
 // softmax's epsilon), concat -> +bias, mean -> head mean via LDS, +bias.
 // Optional lse[r,h] = m + log(l) for the backward pass.
 // ---------------------------------------------------------------------------
-template <int LPE, int HP>
+// LPE (lanes per edge, a power of two <= 64) is a run-time argument: this
+// kernel serves the shapes the lane-group kernel cannot (F % 4 != 0, head
+// means of odd widths), where one instance per head-count class is enough.
+template <int HP>
 __global__ __launch_bounds__(64) void k_edge_fwd(
     const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -30,16 +33,16 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
     const float* __restrict__ s_dst,
     int H, int F, int HF, int concat, int act, float slope, const float* __restrict__ bias,
     float* __restrict__ out, int ld_out, float* __restrict__ lse, DropArgs drop_arg,
-    float* __restrict__ y_heads) {
+    float* __restrict__ y_heads, int LPE) {
     const DropArgs drop = resolve_drop(drop_arg);
     constexpr int C = (512 / HP) < kWave ? (512 / HP) : kWave;  // edges per chunk
     constexpr int R = C * HP / kWave;                          // score slots per lane
-    constexpr int EPI = kWave / LPE;                           // edges per gather step
-    constexpr int U = (EPI >= 16) ? 2 : 4;                     // gather steps in flight
+    constexpr int U = 4;                                       // gather steps in flight
+    const int EPI = kWave / LPE;                               // edges per gather step
     __shared__ int col_s[C];
     __shared__ float p_s[C * HP];
     __shared__ float hv_s[HP];
-    __shared__ float y_s[LPE * 4];
+    __shared__ float y_s[kWave * 4];
 
     const int lane = threadIdx.x;
     const int pos = row_begin + blockIdx.x;
@@ -130,7 +133,6 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 
 #pragma unroll
     for (int off = HP; off < kWave; off <<= 1) l_run += __shfl_xor(l_run, off);
-#pragma unroll
     for (int off = LPE; off < kWave; off <<= 1) {
         acc.x += __shfl_xor(acc.x, off);
         acc.y += __shfl_xor(acc.y, off);
@@ -196,7 +198,7 @@ __global__ __launch_bounds__(64) void k_edge_fwd(
 //   * multi-GPU passes (distributed.py): pass c covers the sources that arrived
 //     with all-gather chunk c, loading the state pass c-1 stored;
 //   * hub rows (degree skew): the segments of one long row run in parallel as
-//     separate "virtual rows", and k_edge_merge combines their states.
+//     separate "virtual rows", and k_edge_merge_wg combines their states.
 // ---------------------------------------------------------------------------
 
 // KINK (training forward, recompute backward): also the per-head "kink sums"
@@ -687,157 +689,6 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     }
 }
 
-#ifdef GAT_AB_KERNELS  // measured and not adopted (profiles/r04/edge_ab_lds_*.json); tools-only build
-// ---------------------------------------------------------------------------
-// LDS-staged variant of k_edge_grp for short rows (north_star's "LDS staging of
-// neighbor Wh tiles per wavefront"; A/B knob GAT_EDGE_LDSDMA=1).  Same lane
-// groups (G lanes = one 128-B plane row or 256-B row, one float4 per lane,
-// U = 4 in-edges per chunk), but the source rows are not gathered into
-// registers: they arrive in a per-wave LDS ring by LDS-DMA
-// (global_load_lds_dwordx4, one wave-instruction per edge slot of the chunk:
-// lane l's 16 B of its row land at ring + 16 l), and so do the column
-// indices (global_load_lds_dword, G/U chunks per instruction).  With no VGPRs
-// held by loads in flight, every wave keeps D = 2 chunks of rows (and 3-5
-// chunks of indices) in flight while it scores and accumulates one chunk
-// read back from LDS.  The per-lane arithmetic is k_edge_grp's (fused source
-// score in log2 units, online softmax, concat + bias).  Eval only: no
-// dropout, no carried segment state, no Kahan rows (the launcher takes it
-// for short-row graphs only).  Ordering: every LDS read of a ring slot
-// follows a counted s_waitcnt vmcnt that retires that slot's DMAs (younger
-// DMAs may stay in flight); a slot is refilled one chunk after it was read.
-// ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void* edge_lds_ptr;
-
-__device__ __forceinline__ void edge_dma16(const float* src, void* lds_dst) {
-    const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(edge_lds_ptr)lds_dst);
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(src), "s"(l)
-        : "memory");
-}
-
-__device__ __forceinline__ void edge_dma4(const int* src, void* lds_dst) {
-    const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(edge_lds_ptr)lds_dst);
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-        "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(src), "s"(l)
-        : "memory");
-}
-
-template <int G>
-__global__ __launch_bounds__(256) void k_edge_lds(
-    const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
-    int row_begin, int row_end, const float* __restrict__ Wh, int ld_wh,
-    const float* __restrict__ a_src, const float* __restrict__ c_src,
-    const float* __restrict__ s_dst, int H, int F, int HF, float slope,
-    const float* __restrict__ bias, float* __restrict__ out, int ld_out, int nslices,
-    int slice_w, long long slice_stride, int store_wt) {
-    constexpr int U = 4;
-    constexpr int CPD = G / U;        // chunks of indices per index DMA
-    constexpr int NB = 3;             // row ring: D = 2 chunks in flight + 1 read
-    constexpr int NC = 4;             // index ring (in index-DMA units)
-    __shared__ __attribute__((aligned(16))) float rowring[4][NB][U][kWave * 4];
-    __shared__ __attribute__((aligned(16))) int colring[4][NC][kWave];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane & (G - 1), grp = lane / G;
-    const int sl = nslices > 1 ? (int)(blockIdx.x % (unsigned)nslices) : 0;
-    const unsigned blk = nslices > 1 ? blockIdx.x / (unsigned)nslices : blockIdx.x;
-    const int pos0 = row_begin + (int)((blk * (size_t)blockDim.x + threadIdx.x) / G);
-    const bool live = pos0 < row_end;
-    const int pos = live ? pos0 : row_end - 1;  // dead groups shadow a live row, store nothing
-    const int r = order != nullptr ? order[pos] : pos;
-    const int loff = 4 * c;                     // < slice width: G * 4 == row floats
-    const int coff = sl * slice_w + loff;
-    const float* __restrict__ Whs = Wh + (size_t)sl * (size_t)slice_stride + loff;
-    const int h = coff / F;
-    const f32x4 a4 = *reinterpret_cast<const f32x4*>(a_src + coff) * kLog2e;
-    const float c1 = c_src[h];
-    const int si = er.by_pos ? pos : r;
-    const int e0 = er.eb[si], e1 = er.ee[si];
-    const int len = e1 - e0;
-    const float sd = (s_dst[(size_t)r * H + h] + c1) * kLog2e;
-    // chunks this wave walks: the longest of its rows (rows are degree-ordered)
-    int nch = (len + U - 1) / U;
-#pragma unroll
-    for (int off = G; off < kWave; off <<= 1) nch = max(nch, __shfl_xor(nch, off));
-    const int elast = e1 > e0 ? e1 - 1 : (e0 > 0 ? e0 - 1 : 0);  // a valid index position
-    // index DMA for index block q (chunks q*CPD .. q*CPD+CPD-1 of every row)
-    auto fetch_cols = [&](int q) {
-        const int e = min(e0 + (q * CPD + c / U) * U + (c % U), elast);
-        edge_dma4(col + e, &colring[w][q % NC][0]);
-    };
-    // row DMAs of chunk k: slot u for all groups of the wave
-    auto fetch_rows = [&](int k) {
-        const int* cw = &colring[w][(k / CPD) % NC][grp * G + (k % CPD) * U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) edge_dma16(Whs + (size_t)cw[u] * ld_wh, &rowring[w][k % NB][u][0]);
-    };
-    // prologue: indices of chunks 0 .. 3*CPD-1, then rows of chunks 0 and 1
-    fetch_cols(0);
-    fetch_cols(1);
-    fetch_cols(2);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    fetch_rows(0);
-    fetch_rows(1);
-    float m = -INFINITY, l = 0.f;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < nch; ++k) {
-        // indices CPD*3 chunks ahead (their DMA retires behind the row DMAs the
-        // waits below retire); rows 2 chunks ahead
-        if (k % CPD == 0) fetch_cols(k / CPD + 3);
-        fetch_rows(k + 2);  // past the row end: clamped indices, unused
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * U) : "memory");
-        const int nk = min(U, e1 - (e0 + k * U));
-        if (nk > 0) {
-            f32x4 v[U];
-            float sc[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                v[u] = *reinterpret_cast<const f32x4*>(&rowring[w][k % NB][u][4 * lane]);
-                f32x2 d2 = f32x2{v[u].x, v[u].y} * f32x2{a4.x, a4.y};
-                d2 += f32x2{v[u].z, v[u].w} * f32x2{a4.z, a4.w};
-                sc[u] = d2.x + d2.y;
-            }
-            const int hl = F / 4;
-            if (hl > 1) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) sc[u] = group_sum16(sc[u], hl);
-            }
-            float emax = -INFINITY;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const float z = sd + sc[u];
-                sc[u] = u < nk ? fmaxf(z, z * slope) : -INFINITY;
-                emax = fmaxf(emax, sc[u]);
-            }
-            const float m_new = fmaxf(m, emax);
-            const float scale = __builtin_amdgcn_exp2f(m - m_new);
-            l *= scale;
-            acc *= scale;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const float p = __builtin_amdgcn_exp2f(sc[u] - m_new);
-                l += p;
-                acc += p * v[u];
-            }
-            m = m_new;
-        }
-    }
-    // the row DMAs issued past the last chunk must land before the LDS is released
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!live) return;
-    const float inv = 1.f / (l + 1e-16f);
-    const f32x4 b = *reinterpret_cast<const f32x4*>(bias + coff);
-    store_out4(out, (size_t)r * ld_out + coff, acc * inv + b, store_wt);
-}
-
-#endif  // GAT_AB_KERNELS
 
 // ---------------------------------------------------------------------------
 // Merge of split hub rows (degree skew).  A target row with more in-edges
@@ -845,68 +696,15 @@ __global__ __launch_bounds__(256) void k_edge_lds(
 // separate virtual rows of k_edge_grp (EdgeRows by_pos + store), in parallel;
 // hub k's segment states are virtual rows [vptr[k], vptr[k+1]) (through
 // vslot when given: segment j's state at vslot[j], the schedule position the
-// segment ran at when the segments are not scheduled hub by hub).  Per head:
+// segment ran at).  Per head:
 //   M = max_s m_s,  L = sum_s l_s 2^(m_s - M),  y = sum_s acc_s 2^(m_s - M) / (L + 1e-16)
 // which is the segmented softmax of PyG utils.softmax (GAT.py:60) regrouped.
-// One wave per hub row; the segment loop is short (<= a few hundred).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_edge_merge(
-    const int* __restrict__ hub_rows, const int* __restrict__ vptr,
-    const int* __restrict__ vslot, int n_hub,
-    const float* __restrict__ st_acc, int ld_st, const float* __restrict__ st_ml, int H, int F,
-    int HF, int concat, const float* __restrict__ bias, float* __restrict__ out, int ld_out,
-    float* __restrict__ lse, float* __restrict__ y_heads) {
-    __shared__ float Ms[GAT_MAX_HEADS], Ls[GAT_MAX_HEADS], ys[GAT_MAX_HF];
-    const int k = blockIdx.x;
-    if (k >= n_hub) return;
-    const int lane = threadIdx.x;
-    const int r = hub_rows[k], s0 = vptr[k], s1 = vptr[k + 1];
-#define SLOT(sg) (vslot != nullptr ? vslot[sg] : (sg))
-    for (int h = lane; h < H; h += kWave) {
-        float M = -INFINITY;
-        for (int sg = s0; sg < s1; ++sg) M = fmaxf(M, st_ml[(size_t)SLOT(sg) * 2 * H + h]);
-        float L = 0.f;
-        for (int sg = s0; sg < s1; ++sg) {
-            const float ms = st_ml[(size_t)SLOT(sg) * 2 * H + h];
-            if (ms != -INFINITY) L += st_ml[(size_t)SLOT(sg) * 2 * H + H + h] * __builtin_amdgcn_exp2f(ms - M);
-        }
-        Ms[h] = M;
-        Ls[h] = L;
-        if (lse != nullptr) lse[(size_t)r * H + h] = (M + log2f(L)) * kLn2;
-    }
-    __syncthreads();
-    for (int cc = lane; cc < HF; cc += kWave) {
-        const int h = cc / F;
-        const float M = Ms[h];
-        float a = 0.f;
-        for (int sg = s0; sg < s1; ++sg) {
-            const float ms = st_ml[(size_t)SLOT(sg) * 2 * H + h];
-            if (ms != -INFINITY) a += st_acc[(size_t)SLOT(sg) * ld_st + cc] * __builtin_amdgcn_exp2f(ms - M);
-        }
-        const float y = a / (Ls[h] + 1e-16f);
-        if (y_heads != nullptr) y_heads[(size_t)r * HF + cc] = y;
-        if (concat) out[(size_t)r * ld_out + cc] = y + bias[cc];
-        else ys[cc] = y;
-    }
-    if (!concat) {
-        __syncthreads();
-        for (int f = lane; f < F; f += kWave) {
-            float sum = 0.f;
-            for (int h = 0; h < H; ++h) sum += ys[h * F + f];
-            out[(size_t)r * ld_out + f] = sum / (float)H + bias[f];
-        }
-    }
-#undef SLOT
-}
-
-// The same merge with a hub's segments spread over a 256-thread workgroup
-// (the default since round 5).  k_edge_merge walks all of a hub's segments in
-// one lane per head / column, three dependent loops of one load each: at
-// power-law Reddit (3.4k hubs, up to 116 segments) its launch took 120 us, set
-// by the longest hubs' load chains.  Here thread t takes segments
+// A hub's segments are spread over a 256-thread workgroup (round 5: a
+// one-wave-per-hub merge walking all of a hub's segments in one lane per head
+// / column, three dependent loops of one load each, took 120 us at power-law
+// Reddit, set by the longest hubs' load chains).  Thread t takes segments
 // s0 + g, s0 + g + ng, ... (g = t / H or t / HF), and the per-group partial
-// maxima / sums are combined in LDS in group order: deterministic, the same
-// segmented softmax regrouped as k_edge_merge (sums in another order).
+// maxima / sums are combined in LDS in group order (deterministic).
 __global__ __launch_bounds__(256) void k_edge_merge_wg(
     const int* __restrict__ hub_rows, const int* __restrict__ vptr,
     const int* __restrict__ vslot, int n_hub,
@@ -988,141 +786,121 @@ __global__ __launch_bounds__(256) void k_edge_merge_wg(
 
 }  // namespace
 
-// Fused lane-group edge kernel, optionally with the gathers pipelined one
-// chunk ahead (GAT_EDGE_PIPE A/B knob): instantiated for the (U, V) pairs the
-// default schedule uses.
-// the fused kernel with the head's lane count hl as a constant where the
-// lane group is one of HF = 64's (G = 4, 8, 16: planes or rows, V = 1 or 2)
-// and hl is 1 or 2 (heads of 4 or 8 columns); the run-time form otherwise.
-// GAT_EDGE_HL=0 (A/B knob) forces the run-time form.
+// ---------------------------------------------------------------------------
+// Which k_edge_grp instances exist (the dispatch below maps every request onto
+// one of them; the round-5 library carried 261 instances, most reachable only
+// through A/B knobs):
+//   * the "fast" lane groups G = 4, 8, 16 at V = 1 and G = 4, 8 at V = 2 — the
+//     reference's HF = 32 / 64 rows and 128-B plane rows — with heads of 4 or 8
+//     columns per lane group (hl = 1, 2 as a constant, HL): U = 4 (row-batched
+//     col values RC where rows average >= 16 in-edges), 8 and 16; two or four
+//     lane groups per row for small launches (S, G = 8 / 16, V = 1, U <= 8);
+//     the pipelined long-row kernel (V = 2, U = 16); the kink-sum training
+//     forward on HF = 64 (G = 16 at V = 1, G = 8 at V = 2);
+//   * other head widths on those groups (hl read at run time): U = 8 only;
+//   * every other lane group (HF = 4, 8, 128, 256; G = 16 at V = 2): U = 8;
+//   * the gathered-score form (head lanes not a power of two): V = 1, U = 8;
+//   * the small-Fin fused forward (XF): G = 8 / 16, hl 1 / 2, U = 4, fin 1-4.
 // The row-batched col form (RC) for rows of >= 16 in-edges on average (PPI:
 // edge kernel 26.3 -> 25.2 us, same box, profiles/r05/edge_ab_rowcol_ppi.json);
 // rows of 2-3 chunks (arxiv, CIFAR) keep the one-chunk-ahead loads, which
 // there measured faster (arxiv 54.0 vs 55.9 us, CIFAR H=8 18.8 vs 20.2;
-// profiles/r05/edge_ab_rowcol_ungated_*.json).
-// GAT_EDGE_ROWCOL=0 (A/B knob): never.
+// profiles/r05/edge_ab_rowcol_ungated_*.json).  GAT_EDGE_ROWCOL=0 (knob):
+// never.  (Gathers one chunk ahead on top of it, round 6: 26.1 vs 25.1 us at
+// PPI, 100 VGPRs; profiles/r06/edge_ab_rc_pipelined_ppi.json; removed.)
+// ---------------------------------------------------------------------------
 static bool rowcol_for(int edges_per_row_hint) {
     const char* v = knob("GAT_EDGE_ROWCOL");
     return (v == nullptr || std::atoi(v) != 0) && edges_per_row_hint >= 16;
 }
 
-template <int G, int U, int V, bool PIPE, bool KINK, int S, class... A>
-static void launch_grp_hl(int hl, bool rc, dim3 grid, dim3 block, size_t lds, hipStream_t st,
-                          A... a) {
-    if constexpr (U == 4 && G >= 4 && S == 1 && !PIPE) {
-        if (rc) {
-            if constexpr (G == 4 || G == 8 || G == 16) {
-                const char* v = knob("GAT_EDGE_HL");
-                const bool on = v == nullptr || std::atoi(v) != 0;
-                if (on && hl == 1) {
-                    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1, 0, 1>), grid,
-                                       block, lds, st, a...);
-                    return;
-                }
-                if (on && hl == 2) {
-                    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 2, 0, 1>), grid,
-                                       block, lds, st, a...);
-                    return;
-                }
+constexpr bool fast_group(int g, int v) { return (g == 4 || g == 8 || g == 16) && (v == 1 || g <= 8); }
+
+// one launch of the fused kernel with the head's lane count as a constant
+// (hl = 1 or 2) or read at run time (HL = 0)
+template <int G, int U, int V, bool PIPE, bool KINK, int S, int RC, class... A>
+static void launch_hl(int hl, dim3 grid, dim3 block, hipStream_t st, A... a) {
+    if constexpr (fast_group(G, V)) {
+        if (hl == 1) {
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1, 0, RC>), grid, block, 0,
+                               st, a...);
+            return;
+        }
+        if (hl == 2) {
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 2, 0, RC>), grid, block, 0,
+                               st, a...);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 0, 0, RC>), grid, block, 0, st,
+                       a...);
+}
+
+// the fused kernel on a fast lane group; u, rc, pipe and split as the
+// dispatch resolved them (edge_aggregate_impl)
+template <int G, int V, bool KINK, class... A>
+static void launch_fast(int u, int rc, int pipe, int split, int hl, dim3 grid, dim3 block,
+                        hipStream_t st, A... a) {
+    constexpr bool kink_ok = (G == 16 && V == 1) || (G == 8 && V == 2);
+    if constexpr (!KINK || kink_ok) {
+        constexpr bool splittable = !KINK && V == 1 && (G == 8 || G == 16);
+        if (u == 4) {
+            if constexpr (splittable) {
+                if (split == 2) return launch_hl<G, 4, V, false, false, 2, 0>(hl, dim3(grid.x * 2), block, st, a...);
+                if (split == 4) return launch_hl<G, 4, V, false, false, 4, 0>(hl, dim3(grid.x * 4), block, st, a...);
             }
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 0, 0, 1>), grid, block,
-                               lds, st, a...);
-            return;
+            if constexpr (G != 4) {  // (row-batched ids: G = 8, 16)
+                if (rc) return launch_hl<G, 4, V, false, KINK, 1, 1>(hl, grid, block, st, a...);
+            }
+            return launch_hl<G, 4, V, false, KINK, 1, 0>(hl, grid, block, st, a...);
         }
+        if (u == 8) {
+            if constexpr (splittable) {
+                if (split == 2) return launch_hl<G, 8, V, false, false, 2, 0>(hl, dim3(grid.x * 2), block, st, a...);
+                if (split == 4) return launch_hl<G, 8, V, false, false, 4, 0>(hl, dim3(grid.x * 4), block, st, a...);
+            }
+            return launch_hl<G, 8, V, false, KINK, 1, 0>(hl, grid, block, st, a...);
+        }
+        if constexpr (V == 2) {
+            if (pipe) return launch_hl<G, 16, V, true, KINK, 1, 0>(hl, grid, block, st, a...);
+        }
+        launch_hl<G, 16, V, false, KINK, 1, 0>(hl, grid, block, st, a...);
     }
-    if constexpr (G == 4 || G == 8 || G == 16) {
-        const char* v = knob("GAT_EDGE_HL");
-        const bool on = v == nullptr || std::atoi(v) != 0;
-        if (on && hl == 1) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1>), grid, block, lds, st, a...);
-            return;
-        }
-        if (on && hl == 2) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 2>), grid, block, lds, st, a...);
-            return;
-        }
-    }
-    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 0>), grid, block, lds, st, a...);
 }
 
-template <int G, int U, int V, bool KINK = false, class... A>
-static void launch_edge_fused(int pipe, int split, int hl, bool rc, dim3 grid, dim3 block,
-                              hipStream_t st, A... a) {
-    // GAT_EDGE_LDS (A/B knob): dynamic LDS bytes per block, unused by the
-    // kernel — caps the blocks resident per CU (160 KB / bytes)
-    size_t lds = 0;
-    if (const char* el = knob("GAT_EDGE_LDS")) lds = (size_t)std::atol(el);
-    // the pipelined form is instantiated for the pair the default schedule
-    // pipelines (U = 16, V = 2: Reddit-scale rows) and U = 8 at V = 2 (GAT_EDGE_PIPE
-    // A/B); elsewhere the knob is ignored.  (Short-row chunks at V = 1 were
-    // pipelined too in round 4 and measured slower: PPI 26.9 -> 27.5 us, arxiv
-    // 54.0 -> 54.9 us, CIFAR equal; profiles/r05/edge_ab_pipe_short_*.json)
-    if constexpr (V == 2 && (U == 16 || U == 8)) {
-        if (pipe) {
-            launch_grp_hl<G, U, V, true, KINK, 1>(hl, rc, grid, block, lds, st, a...);
-            return;
-        }
-    }
-    // two or four lane groups per row (S = split, GAT_EDGE_SPLIT): instantiated
-    // for the short-row lane groups of HF = 64 (G = 8: 2-plane table; G = 16:
-    // row-major)
-    if constexpr (!KINK && V == 1 && U <= 8 && (G == 8 || G == 16)) {
-        if (split == 2) {
-            launch_grp_hl<G, U, V, false, false, 2>(hl, rc, dim3(grid.x * 2), block, lds, st, a...);
-            return;
-        }
-        if (split == 4) {
-            launch_grp_hl<G, U, V, false, false, 4>(hl, rc, dim3(grid.x * 4), block, lds, st, a...);
-            return;
-        }
-    }
-    launch_grp_hl<G, U, V, false, KINK, 1>(hl, rc, grid, block, lds, st, a...);
-}
-
-// the small-Fin fused forward (XF): lane groups of HF = 32 or 64 (G = 8, 16),
-// heads of 4 or 8 columns, U = 4 or 8, fin 1-4
-template <int G, int U, int HL, class... A>
-static void launch_xf_fin(int xf, bool rc, dim3 grid, dim3 block, hipStream_t st, A... a) {
-#define GAT_XF(N)                                                                               \
-    if (U == 4 && rc)                                                                           \
-        hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, N, U == 4 ? 1 : 0>), \
-                           grid, block, 0, st, a...);                                           \
-    else                                                                                        \
-        hipLaunchKernelGGL((k_edge_grp<G, U, 1, true, false, false, 1, HL, N>), grid, block,    \
-                           0, st, a...)
+// the small-Fin fused forward (XF = fin, 1-4): G = 8 or 16, hl 1 or 2, U = 4
+template <int G, int HL, class... A>
+static void launch_xf(int xf, dim3 grid, dim3 block, hipStream_t st, A... a) {
     switch (xf) {
-        case 1: GAT_XF(1); break;
-        case 2: GAT_XF(2); break;
-        case 3: GAT_XF(3); break;
-        default: GAT_XF(4); break;
-    }
-#undef GAT_XF
-}
-
-template <int G, class... A>
-static void launch_xf(int u, int hl, int xf, bool rc, dim3 grid, dim3 block, hipStream_t st,
-                      A... a) {
-    if (u == 4) {
-        if (hl == 1) launch_xf_fin<G, 4, 1>(xf, rc, grid, block, st, a...);
-        else launch_xf_fin<G, 4, 2>(xf, rc, grid, block, st, a...);
-    } else {
-        if (hl == 1) launch_xf_fin<G, 8, 1>(xf, false, grid, block, st, a...);
-        else launch_xf_fin<G, 8, 2>(xf, false, grid, block, st, a...);
+        case 1: hipLaunchKernelGGL((k_edge_grp<G, 4, 1, true, false, false, 1, HL, 1>), grid, block, 0, st, a...); break;
+        case 2: hipLaunchKernelGGL((k_edge_grp<G, 4, 1, true, false, false, 1, HL, 2>), grid, block, 0, st, a...); break;
+        case 3: hipLaunchKernelGGL((k_edge_grp<G, 4, 1, true, false, false, 1, HL, 3>), grid, block, 0, st, a...); break;
+        default: hipLaunchKernelGGL((k_edge_grp<G, 4, 1, true, false, false, 1, HL, 4>), grid, block, 0, st, a...); break;
     }
 }
 
-// the kink-sum forward is instantiated for the lane groups of HF = 64 heads
-// (G = 16 at V = 1, G = 8 at V = 2); kink_grp_ok says which launch it serves
-static bool kink_grp_ok(int g, int v) { return (g == 16 && v == 1) || (g == 8 && v == 2); }
+// the shapes the small-Fin fused forward (XF) takes: fin 1-4, heads of 4 or 8
+// columns (hl = 1, 2 at V = 1), lane groups of 8 or 16 (HF 17-64), LeakyReLU
+// with a slope in [0, 1]
+static bool xf_shape_ok(int fin, int heads, int f, float slope) {
+    if (fin <= 0 || fin > 4 || heads <= 0 || f <= 0 || f % 4 != 0) return false;
+    const int hf = heads * f, hl = f / 4, g = next_pow2((hf + 3) / 4);
+    return hf <= GAT_MAX_HF && heads <= GAT_MAX_HEADS && (hl == 1 || hl == 2) &&
+           (g == 8 || g == 16) && slope >= 0.f && slope <= 1.f;
+}
 
-template <int G, int U, int V, class... A>
-static void launch_edge_kink(int pipe, int hl, bool rc, dim3 grid, dim3 block, hipStream_t st,
-                             A... a) {
-    if constexpr ((G == 16 && V == 1) || (G == 8 && V == 2))
-        launch_edge_fused<G, U, V, true>(pipe, 1, hl, rc, grid, block, st, a...);
+// gat_layer_forward's choice (GAT_EDGE_XPROJ=0, knob: never fuse)
+static bool xproj_takes(int n, int fin, int heads, int f, float slope) {
+    const char* v = knob("GAT_EDGE_XPROJ");
+    return n > 0 && (v == nullptr || std::atoi(v) != 0) && xf_shape_ok(fin, heads, f, slope);
 }
 
 extern "C" {
+
+int gat_layer_forward_fuses(int n, int fin, int heads, int f, int concat, float negative_slope) {
+    (void)concat;  // (a head mean of heads of 4 or 8 columns fuses too)
+    return xproj_takes(n, fin, heads, f, negative_slope) ? 1 : 0;
+}
 
 static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row_order,
                                int row_begin, int row_end, const float* wh, int ld_wh,
@@ -1153,7 +931,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     const int slice_w = sliced ? ld_wh : round_up4(hf);
     // write-through output stores: only for the final (eval) output, which the
     // next kernel reads, not for the training forward's extra tensors
-    const int store_wt = (lse == nullptr && q_heads == nullptr) ? store_wt_on() : 0;
+    const int store_wt = (lse == nullptr && q_heads == nullptr) ? 1 : 0;
     if (s_src != nullptr && ld_s < heads) return GAT_EINVAL;
     const bool have_a = a_src != nullptr && c_src != nullptr;
     if (s_src == nullptr && !have_a) return GAT_EINVAL;
@@ -1179,30 +957,31 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     if (local_hint && !sliced && round_up4(hf) <= 32) vv = 2;
     if (const char* ev = knob("GAT_EDGE_V")) vv = std::atoi(ev) >= 2 ? 2 : 1;
     if (xp != nullptr) vv = 1;  // the small-Fin form: four columns per lane
-
     while (vv > 1 && f % (4 * vv) != 0) vv >>= 1;
+    // fused source score: the head's lanes must form an aligned power-of-two
+    // block; otherwise (concat only) the gathered-score form at V = 1
+    if (vv > 1 && !(next_pow2(f / (4 * vv)) == f / (4 * vv) && have_a)) vv = 1;
     const int hl = f / (4 * vv);  // lanes per head
     const bool pow2_hl = (f % (4 * vv) == 0) && next_pow2(hl) == hl;
     const int gcols = sliced ? slice_w : hf;  // columns one lane group owns
     const int g = next_pow2((gcols + 4 * vv - 1) / (4 * vv));
-    const bool grp_ok = (f % 4 == 0) && (concat || pow2_hl) && slope_ok;
-    // fused source score: the head's lanes must form an aligned power-of-two block
-    bool fused = grp_ok && pow2_hl && have_a;
-    if (fused && s_src != nullptr) fused = kernel_choice("GAT_EDGE_SCORE", "gather");
+    const bool grp_ok = (f % 4 == 0) && (concat || pow2_hl) && slope_ok && g <= kWave;
+    const bool fused = grp_ok && pow2_hl && have_a;
     if (s_src == nullptr && !fused) return GAT_EUNSUPPORTED;
     const bool kink = q_heads != nullptr;
+    const bool kink_grp = (g == 16 && vv == 1) || (g == 8 && vv == 2);
     if (kink && (!fused || sliced || r_heads == nullptr || lse == nullptr || y_heads == nullptr ||
-                 er.by_pos || er.load || er.store_lt > 0))
+                 er.by_pos || er.load || er.store_lt > 0 || !kink_grp))
         return GAT_EUNSUPPORTED;
     // a slice holds whole heads (the fused score sums a head inside one group)
     if (sliced && (!fused || slice_w % f != 0)) return GAT_EUNSUPPORTED;
-    if (grp_ok && (s_src == nullptr || kernel_choice("GAT_EDGE_KERNEL", "generic"))) {
+    if (grp_ok) {
         // edges per chunk: short rows want short chunks (less padding), long rows
         // more loads in flight; GAT_EDGE_U overrides
         // (tools/tune_edge.py: PPI, ~28 per row, 36.9 us at U = 8 -> 33.1 us at U = 4)
         int u = edges_per_row_hint <= 0 ? 8 : edges_per_row_hint <= 32 ? 4
               : edges_per_row_hint <= 64 ? 8 : 16;
-        if (const char* eu = knob("GAT_EDGE_U")) u = std::atoi(eu);
+        if (const char* eu = knob("GAT_EDGE_U")) u = std::atoi(eu) >= 16 ? 16 : std::atoi(eu) <= 4 ? 4 : 8;
         const long long threads = (long long)rows * g;
         const long long blocks = ((threads + 255) / 256) * nslices;
         if (blocks >= (1LL << 31)) return GAT_EUNSUPPORTED;
@@ -1218,13 +997,12 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // unsplit pass 252 vs 292; tools/emu_probe.py, profiles/r04/emu_reddit_p8.json)
         const bool seg_pass = !er.by_pos && (er.load || er.store_lt > 0);
         int pipe = (u == 16 && vv == 2 && !seg_pass) ? 1 : 0;
-        if (const char* ep = knob("GAT_EDGE_PIPE")) pipe = std::atoi(ep);
-        // two lane groups per row (the grid doubles inside launch_edge_fused):
-        // GAT_EDGE_SPLIT = 2 (A/B knob); the kink-sum forward and the pipelined
-        // kernel keep one group.  Segment passes (er.load / store_lt: hub
-        // segments, the sharded chunk passes) DO take S = 2/4: the carried
-        // (m, l, acc) state is loaded into group 0, merged across the groups in
-        // registers, and stored by group 0.
+        if (const char* ep = knob("GAT_EDGE_PIPE")) pipe = std::atoi(ep) != 0 && u == 16 && vv == 2;
+        // two lane groups per row (the grid doubles inside launch_fast); the
+        // kink-sum forward and the pipelined kernel keep one group.  Segment
+        // passes (er.load / store_lt: hub segments, the sharded chunk passes) DO
+        // take S = 2/4: the carried (m, l, acc) state is loaded into group 0,
+        // merged across the groups in registers, and stored by group 0.
         // Default: launches of fewer than ~4 waves per SIMD (a rank's share of a
         // small graph: PPI at P = 4 / 8 edge passes 14.2 -> 11.3 / 13.3 -> 9.0 us,
         // tools/emu_probe.py) — there the per-row chain of dependent chunk loads
@@ -1233,28 +1011,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         // waves per SIMD (PPI at P = 8: 9.0 -> 8.2 us; at P = 4 it is 13.6).
         // Rows of fewer than ~3 chunks per group gain nothing from a split (arxiv
         // at P = 8, 8 edges per row: 10.9 us whole, 12.0 / 15.8 split 2 / 4).
-#ifdef GAT_AB_KERNELS
-        // GAT_EDGE_LDSDMA=1 (A/B knob): the LDS-staged short-row kernel
-        // (k_edge_lds) where it applies: eval, concat, fused score, U = 4,
-        // one float4 per lane, a lane group = one 128-B plane row or 256-B row
-        if (const char* ld = knob("GAT_EDGE_LDSDMA")) {
-            if (std::atoi(ld) == 1 && fused && vv == 1 && u == 4 && !kink && concat &&
-                !er.load && er.store_lt == 0 && drop.thresh == 0 && lse == nullptr &&
-                y_heads == nullptr && (g == 8 || g == 16) && 4 * g == gcols) {
-                if (g == 8)
-                    hipLaunchKernelGGL((k_edge_lds<8>), grid, block, 0, st, er, col, row_order,
-                                       row_begin, row_end, wh, ld_wh, a_src, c_src, s_dst, heads,
-                                       f, hf, negative_slope, bias, out, ld_out, nslices, slice_w,
-                                       slice_stride, store_wt);
-                else
-                    hipLaunchKernelGGL((k_edge_lds<16>), grid, block, 0, st, er, col, row_order,
-                                       row_begin, row_end, wh, ld_wh, a_src, c_src, s_dst, heads,
-                                       f, hf, negative_slope, bias, out, ld_out, nslices, slice_w,
-                                       slice_stride, store_wt);
-                return status_of(hipGetLastError());
-            }
-        }
-#endif
+        // GAT_EDGE_SPLIT (knob) forces 1, 2 or 4.
         const long long waves = (long long)rows * g * nslices / kWave;
         const int chunks = edges_per_row_hint > 0 ? edges_per_row_hint / u : 1 << 20;
         int split = (waves < 2048 && chunks >= 6) ? 4 : (waves < 4096 && chunks >= 3) ? 2 : 1;
@@ -1264,8 +1021,18 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         }
         if (kink || pipe) split = 1;
         if ((long long)blocks * split >= (1LL << 31)) split = 1;
-        if (kink && !kink_grp_ok(g, vv)) return GAT_EUNSUPPORTED;
-        const bool rc = rowcol_for(edges_per_row_hint);
+        bool rc = rowcol_for(edges_per_row_hint);
+        // the instances that exist (see above): everything off the fast lane
+        // groups, other head widths and the gathered-score form run U = 8, one
+        // group per row, no row-batched ids, no pipelining
+        const bool fast = fused && fast_group(g, vv) && (hl == 1 || hl == 2);
+        if (!fast) {
+            u = 8;
+            split = 1;
+            pipe = 0;
+        }
+        if (vv == 2 && u == 8) u = 4;  // V = 2 below U = 16: local narrow rows
+        if (u != 4 || g == 4) rc = false;
         const XProjArgs xpa = xp != nullptr ? *xp : XProjArgs{nullptr, nullptr, nullptr, nullptr,
                                                               nullptr, 0};
 #define GAT_GRP_KARGS                                                                         \
@@ -1274,50 +1041,79 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         slice_w, slice_stride, q_heads, r_heads, store_wt, xpa
         if (xp != nullptr) {
             // the small-Fin fused forward: no Wh table, one lane group per row
-            if (!(fused && vv == 1 && !kink && !sliced && (g == 8 || g == 16) &&
-                  (hl == 1 || hl == 2) && xp->fin > 0 && xp->fin <= 4 && (u == 4 || u == 8) &&
-                  xp->x != nullptr && xp->w != nullptr && xp->b != nullptr &&
-                  xp->a_dst != nullptr && xp->c_dst != nullptr))
+            if (!(fused && vv == 1 && !kink && !sliced &&
+                  xf_shape_ok(xp->fin, heads, f, negative_slope) && xp->x != nullptr &&
+                  xp->w != nullptr && xp->b != nullptr && xp->a_dst != nullptr &&
+                  xp->c_dst != nullptr))
                 return GAT_EUNSUPPORTED;
             const int xf = xp->fin;
-            if (g == 8) launch_xf<8>(u, hl, xf, rc, grid, block, st, GAT_GRP_KARGS);
-            else launch_xf<16>(u, hl, xf, rc, grid, block, st, GAT_GRP_KARGS);
+            if (g == 8) {
+                if (hl == 1) launch_xf<8, 1>(xf, grid, block, st, GAT_GRP_KARGS);
+                else launch_xf<8, 2>(xf, grid, block, st, GAT_GRP_KARGS);
+            } else {
+                if (hl == 1) launch_xf<16, 1>(xf, grid, block, st, GAT_GRP_KARGS);
+                else launch_xf<16, 2>(xf, grid, block, st, GAT_GRP_KARGS);
+            }
             return status_of(hipGetLastError());
         }
-#define GAT_GRP_LAUNCH(G, UU, VV)                                                     \
-    if (kink)                                                                         \
-        launch_edge_kink<G, UU, VV>(pipe, hl, rc, grid, block, st, GAT_GRP_KARGS);     \
-    else if (fused)                                                                   \
-        launch_edge_fused<G, UU, VV>(pipe, split, hl, rc, grid, block, st, GAT_GRP_KARGS); \
-    else                                                                              \
-        hipLaunchKernelGGL((k_edge_grp<G, UU, VV, false>), grid, block, 0, st, GAT_GRP_KARGS)
-#define GAT_GRP_U(G, VV)                                                              \
-    if (u == 4) { GAT_GRP_LAUNCH(G, 4, VV); }                                         \
-    else if (u == 16) { GAT_GRP_LAUNCH(G, 16, VV); }                                  \
-    else { GAT_GRP_LAUNCH(G, 8, VV); }
-#define GAT_GRP_G32(VV)                               \
-        case 1: GAT_GRP_U(1, VV) break;               \
-        case 2: GAT_GRP_U(2, VV) break;               \
-        case 4: GAT_GRP_U(4, VV) break;               \
-        case 8: GAT_GRP_U(8, VV) break;               \
-        case 16: GAT_GRP_U(16, VV) break;             \
-        case 32: GAT_GRP_U(32, VV) break;
-        // V = 2 owns <= 256 / 8 = 32 lanes per row: no G = 64 instance
+        if (!fused) {
+            // gathered source scores (V = 1, U = 8)
+#define GAT_GRP_GATHER(G)                                                                     \
+    case G:                                                                                   \
+        hipLaunchKernelGGL((k_edge_grp<G, 8, 1, false>), grid, block, 0, st, GAT_GRP_KARGS);  \
+        break;
+            switch (g) {
+                GAT_GRP_GATHER(1) GAT_GRP_GATHER(2) GAT_GRP_GATHER(4) GAT_GRP_GATHER(8)
+                GAT_GRP_GATHER(16) GAT_GRP_GATHER(32) GAT_GRP_GATHER(64)
+                default: return GAT_EUNSUPPORTED;
+            }
+#undef GAT_GRP_GATHER
+            return status_of(hipGetLastError());
+        }
+        if (fast) {
+            if (vv == 1) {
+                if (g == 4) launch_fast<4, 1, false>(u, rc, pipe, split, hl, grid, block, st, GAT_GRP_KARGS);
+                else if (g == 8) launch_fast<8, 1, false>(u, rc, pipe, split, hl, grid, block, st, GAT_GRP_KARGS);
+                else if (kink) launch_fast<16, 1, true>(u, rc, pipe, split, hl, grid, block, st, GAT_GRP_KARGS);
+                else launch_fast<16, 1, false>(u, rc, pipe, split, hl, grid, block, st, GAT_GRP_KARGS);
+            } else {
+                if (g == 4) launch_fast<4, 2, false>(u, rc, pipe, split, hl, grid, block, st, GAT_GRP_KARGS);
+                else if (kink) launch_fast<8, 2, true>(u, rc, pipe, split, hl, grid, block, st, GAT_GRP_KARGS);
+                else launch_fast<8, 2, false>(u, rc, pipe, split, hl, grid, block, st, GAT_GRP_KARGS);
+            }
+            return status_of(hipGetLastError());
+        }
+        // run-time head width, U = 8, one group per row
+#define GAT_GRP_SLOW(G, VV)                                                                   \
+    if (kink)                                                                                 \
+        hipLaunchKernelGGL((k_edge_grp<G, 8, VV, true, false, (G == 16 && VV == 1) ||          \
+                                                              (G == 8 && VV == 2)>),          \
+                           grid, block, 0, st, GAT_GRP_KARGS);                                \
+    else                                                                                      \
+        hipLaunchKernelGGL((k_edge_grp<G, 8, VV, true>), grid, block, 0, st, GAT_GRP_KARGS)
         if (vv == 2) {
             switch (g) {
-                GAT_GRP_G32(2)
+                case 1: GAT_GRP_SLOW(1, 2); break;
+                case 2: GAT_GRP_SLOW(2, 2); break;
+                case 4: GAT_GRP_SLOW(4, 2); break;
+                case 8: GAT_GRP_SLOW(8, 2); break;
+                case 16: GAT_GRP_SLOW(16, 2); break;
+                case 32: GAT_GRP_SLOW(32, 2); break;
                 default: return GAT_EUNSUPPORTED;
             }
         } else {
             switch (g) {
-                GAT_GRP_G32(1)
-                case 64: GAT_GRP_U(64, 1) break;
+                case 1: GAT_GRP_SLOW(1, 1); break;
+                case 2: GAT_GRP_SLOW(2, 1); break;
+                case 4: GAT_GRP_SLOW(4, 1); break;
+                case 8: GAT_GRP_SLOW(8, 1); break;
+                case 16: GAT_GRP_SLOW(16, 1); break;
+                case 32: GAT_GRP_SLOW(32, 1); break;
+                case 64: GAT_GRP_SLOW(64, 1); break;
                 default: return GAT_EUNSUPPORTED;
             }
         }
-#undef GAT_GRP_G32
-#undef GAT_GRP_U
-#undef GAT_GRP_LAUNCH
+#undef GAT_GRP_SLOW
 #undef GAT_GRP_KARGS
         return status_of(hipGetLastError());
     }
@@ -1327,34 +1123,23 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     const int* rowptr = er.eb;
     const int lpe = next_pow2((round_up4(hf) + 3) / 4);
     const int hp = next_pow2(heads);
+    if (lpe > kWave) return GAT_EUNSUPPORTED;
     const dim3 grid(rows), block(kWave);
-#define GAT_EDGE_LAUNCH(L, P)                                                                \
-    hipLaunchKernelGGL((k_edge_fwd<L, P>), grid, block, 0, st, rowptr, col, row_order,       \
-                       row_begin,                                                            \
-                       row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf, concat, act,    \
-                       negative_slope, bias, out, ld_out, lse, drop, y_heads)
-#define GAT_EDGE_HP(L)                                                                       \
-    switch (hp) {                                                                            \
-        case 1: GAT_EDGE_LAUNCH(L, 1); break;                                                \
-        case 2: GAT_EDGE_LAUNCH(L, 2); break;                                                \
-        case 4: GAT_EDGE_LAUNCH(L, 4); break;                                                \
-        case 8: GAT_EDGE_LAUNCH(L, 8); break;                                                \
-        case 16: GAT_EDGE_LAUNCH(L, 16); break;                                              \
-        case 32: GAT_EDGE_LAUNCH(L, 32); break;                                              \
-        case 64: GAT_EDGE_LAUNCH(L, 64); break;                                              \
-        default: return GAT_EUNSUPPORTED;                                                    \
-    }
-    switch (lpe) {
-        case 1: GAT_EDGE_HP(1) break;
-        case 2: GAT_EDGE_HP(2) break;
-        case 4: GAT_EDGE_HP(4) break;
-        case 8: GAT_EDGE_HP(8) break;
-        case 16: GAT_EDGE_HP(16) break;
-        case 32: GAT_EDGE_HP(32) break;
-        case 64: GAT_EDGE_HP(64) break;
+#define GAT_EDGE_LAUNCH(P)                                                                   \
+    hipLaunchKernelGGL((k_edge_fwd<P>), grid, block, 0, st, rowptr, col, row_order,          \
+                       row_begin, row_end, wh, ld_wh, s_src, ld_s, s_dst, heads, f, hf,      \
+                       concat, act, negative_slope, bias, out, ld_out, lse, drop, y_heads,   \
+                       lpe)
+    switch (hp) {
+        case 1: GAT_EDGE_LAUNCH(1); break;
+        case 2: GAT_EDGE_LAUNCH(2); break;
+        case 4: GAT_EDGE_LAUNCH(4); break;
+        case 8: GAT_EDGE_LAUNCH(8); break;
+        case 16: GAT_EDGE_LAUNCH(16); break;
+        case 32: GAT_EDGE_LAUNCH(32); break;
+        case 64: GAT_EDGE_LAUNCH(64); break;
         default: return GAT_EUNSUPPORTED;
     }
-#undef GAT_EDGE_HP
 #undef GAT_EDGE_LAUNCH
     return status_of(hipGetLastError());
 }
@@ -1448,9 +1233,7 @@ int gat_layer_forward(const float* x, int n, int fin, const float* w, const floa
     // and s_dst are then not written.  GAT_EDGE_XPROJ=0 (A/B knob): project, then
     // aggregate.  Shapes it does not take (GAT_EUNSUPPORTED, nothing launched)
     // take the two-kernel path below.
-    bool xproj_on = fin > 0 && fin <= 4 && x != nullptr && n > 0;
-    if (const char* v = knob("GAT_EDGE_XPROJ")) xproj_on = xproj_on && std::atoi(v) != 0;
-    if (xproj_on) {
+    if (x != nullptr && xproj_takes(n, fin, heads, f, negative_slope)) {
         if (seg_begin == nullptr || seg_end == nullptr || a_src == nullptr || c_src == nullptr)
             return GAT_EINVAL;
         EdgeRows er;
@@ -1540,14 +1323,7 @@ int gat_edge_merge_ex(const int* hub_rows, const int* seg_ptr, const int* seg_sl
     if (hub_rows == nullptr || seg_ptr == nullptr || st_acc == nullptr || st_ml == nullptr ||
         bias == nullptr || out == nullptr)
         return GAT_EINVAL;
-    // GAT_EDGE_MERGE=0 (A/B knob): the one-wave-per-hub merge
-    const char* mk = knob("GAT_EDGE_MERGE");
-    if (mk != nullptr && std::atoi(mk) == 0)
-        hipLaunchKernelGGL(k_edge_merge, dim3(n_hub), dim3(kWave), 0, (hipStream_t)stream,
-                           hub_rows, seg_ptr, seg_slot, n_hub, st_acc, round_up4(hf), st_ml, heads,
-                           f, hf, concat, bias, out, concat ? hf : f, lse, y_heads);
-    else
-        hipLaunchKernelGGL(k_edge_merge_wg, dim3(n_hub), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_edge_merge_wg, dim3(n_hub), dim3(256), 0, (hipStream_t)stream,
                            hub_rows, seg_ptr, seg_slot, n_hub, st_acc, round_up4(hf), st_ml, heads,
                            f, hf, concat, bias, out, concat ? hf : f, lse, y_heads);
     return status_of(hipGetLastError());

@@ -1,6 +1,7 @@
 // MI355X GAT projection: Wh = x W^T + b with the attention scores fused in the
-// epilogue (GAT.py:42-52).  Kernels k_project, k_project_pipe2, k_project_x3,
-// k_project_wres, k_project_wk; C-ABI gat_project, gat_project_sliced.
+// epilogue (GAT.py:42-52).  Kernels k_project, k_project_x3 (+ k_split_w),
+// k_project_wres(_d), k_project_wk; C-ABI gat_project, gat_project_sliced,
+// gat_project_chunked, gat_project_ex.
 
 #include "gat_common.h"
 
@@ -196,168 +197,6 @@ __global__ __launch_bounds__(256) void k_project(
 }
 
 // ---------------------------------------------------------------------------
-// Projection, software-pipelined K loop (Fin > 64).  fp32 MFMA throughput
-// (157 TF) bounds a [N, Fin] x [Fin, 64] projection at large Fin (Reddit:
-// 18 GFLOP -> 115 us).
-//   * block = 128 rows x BN (<= 64) columns; wave w owns rows [32w, 32w+32)
-//     as two 16-row groups, so every W fragment read from LDS feeds two MFMAs;
-//   * per 64-wide K chunk, x [128 x 64] and W [BN x 64] are staged through
-//     LDS with fully coalesced loads, and chunk c+1's loads are in flight in
-//     registers while chunk c's 16 k-steps x 8 MFMAs run; two barriers per
-//     chunk.
-// Per-element overhead (measured against a one-float-per-lane version of the
-// same schedule):
-//   * x and W chunks load LW floats per lane (LW = 4 when fin % 4 == 0, 2 when
-//     fin % 2 == 0) and land in LDS with one ds_write per load — 4x fewer
-//     address computations, loads and LDS writes than one float per lane;
-//     W rows padded to 68 floats (conflict-free B-fragment reads);
-//   * the attention Linears (GAT.py:44-45) reduce over the head's F lanes by
-//     DPP (no LDS permutes), and lane i of the head's group stores row i;
-//   * Wh goes back through an LDS output tile: each thread stores one fixed
-//     float4 column of 8 rows (coalesced rows, row-major or sliced planes).
-// ---------------------------------------------------------------------------
-template <int NT, int LW>
-__global__ __launch_bounds__(256) void k_project_pipe2(
-    const float* __restrict__ X, int n, int fin,
-    const float* __restrict__ W, const float* __restrict__ bW,
-    const float* __restrict__ a1, const float* __restrict__ c1,
-    const float* __restrict__ a2, const float* __restrict__ c2,
-    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
-    float* __restrict__ s_dst, int slice_w, long long slice_stride) {
-    constexpr int BK = 64, KS = BK / 4, BN = NT * 16, BM = 128;
-    constexpr int XS = BK + 4, WS = BK + 4, OS = BN + 4;
-    constexpr int XL = BM * BK / (256 * LW);  // x loads per thread per chunk
-    constexpr int WL = BN * BK / (256 * LW);  // W loads per thread per chunk
-    static_assert(OS <= XS, "the output tile reuses the x tile");
-    using vec = typename std::conditional<LW == 4, f32x4,
-                typename std::conditional<LW == 2, f32x2, float>::type>::type;
-    __shared__ __attribute__((aligned(16))) float wsm[BN * WS];
-    __shared__ __attribute__((aligned(16))) float xsm[BM * XS];
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int cl = lane & 15, kq = lane >> 4;
-    const int blk0 = blockIdx.x * BM;
-    const int row0 = blk0 + w * 32;
-    f32x4 acc[2][NT];
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    vec xn[XL], wn[WL];
-    auto load_chunk = [&](int k0) {
-        // element e = (tid + 256 q) * LW -> row e / 64, k e % 64: consecutive
-        // lanes read consecutive LW-float groups of one row (coalesced).  An LW
-        // group is wholly below or wholly at/after fin (LW divides fin); groups
-        // past fin and rows past n load clamped, in-bounds addresses (their
-        // products meet zeroed W at the LDS write, or feed unstored rows).
-#pragma unroll
-        for (int q = 0; q < XL; ++q) {
-            const int e = (tid + 256 * q) * LW;
-            const int r = min(blk0 + e / BK, n - 1);
-            const int k = min(k0 + e % BK, fin - LW);
-            xn[q] = *reinterpret_cast<const vec*>(X + (size_t)r * fin + k);
-        }
-#pragma unroll
-        for (int q = 0; q < WL; ++q) {
-            const int e = (tid + 256 * q) * LW;
-            const int nn = min(e / BK, HF - 1);
-            const int k = min(k0 + e % BK, fin - LW);
-            wn[q] = *reinterpret_cast<const vec*>(W + (size_t)nn * fin + k);
-        }
-    };
-    load_chunk(0);
-    for (int k0 = 0; k0 < fin; k0 += BK) {
-        __syncthreads();  // the previous chunk's fragment reads are done
-#pragma unroll
-        for (int q = 0; q < XL; ++q) {
-            const int e = (tid + 256 * q) * LW;
-            *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) = xn[q];
-        }
-#pragma unroll
-        for (int q = 0; q < WL; ++q) {
-            const int e = (tid + 256 * q) * LW;
-            const bool ok = e / BK < HF && k0 + e % BK < fin;
-            *reinterpret_cast<vec*>(wsm + (e / BK) * WS + e % BK) = ok ? wn[q] : vec{};
-        }
-        __syncthreads();
-        if (k0 + BK < fin) load_chunk(k0 + BK);  // in flight during this chunk's MFMAs
-        const int ksteps = min(KS, (fin - k0 + 3) / 4);
-        const float* xa0 = xsm + (w * 32 + cl) * XS + kq;
-        const float* xa1 = xa0 + 16 * XS;
-#pragma unroll
-        for (int st = 0; st < KS; ++st) {
-            if (st < ksteps) {  // block-uniform
-                const float a0 = xa0[4 * st], a1v = xa1[4 * st];
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    const float b = wsm[(t * 16 + cl) * WS + 4 * st + kq];
-                    acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][t], 0, 0, 0);
-                    acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v, b, acc[1][t], 0, 0, 0);
-                }
-            }
-        }
-    }
-    __syncthreads();  // x/W tiles dead: the x tile becomes the output tile
-
-    const int hfp = round_up4(HF);
-    const int lf = 31 - __builtin_clz((unsigned)F);  // F is a power of two <= 16
-    float* Os = xsm;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int cc = t * 16 + cl;
-        const float bb = cc < HF ? bW[cc] : 0.f;
-        const float w1 = cc < HF ? a1[cc] : 0.f, w2 = cc < HF ? a2[cc] : 0.f;
-        const int h = cc >> lf, li = cl & (F - 1);
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            float p1[4], p2[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float v = acc[g][t][i] + bb;  // Linear bias inside Wh (GAT.py:43)
-                Os[(w * 32 + 16 * g + kq * 4 + i) * OS + cc] = cc < HF ? v : 0.f;
-                p1[i] = group_sum16(v * w1, F);
-                p2[i] = group_sum16(v * w2, F);
-            }
-            // lane li (< 4) of the head's F lanes stores row kq*4 + li's sums
-            if (li < 4 && li < F && h < H) {
-                const float v1 = li == 0 ? p1[0] : li == 1 ? p1[1] : li == 2 ? p1[2] : p1[3];
-                const float v2 = li == 0 ? p2[0] : li == 1 ? p2[1] : li == 2 ? p2[2] : p2[3];
-                const int rr = row0 + 16 * g + kq * 4 + li;
-                if (rr < n) {
-                    if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = v1 + c1[h];
-                    s_dst[(size_t)rr * H + h] = v2 + c2[h];
-                }
-            }
-            if (F < 4 && li == 0 && h < H) {  // heads narrower than 4 lanes: rows F..3
-#pragma unroll
-                for (int i = 1; i < 4; ++i) {
-                    const int rr = row0 + 16 * g + kq * 4 + i;
-                    if (i >= F && rr < n) {
-                        if (Ss != nullptr) Ss[(size_t)rr * ld_s + h] = p1[i] + c1[h];
-                        s_dst[(size_t)rr * H + h] = p2[i] + c2[h];
-                    }
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // Wh stores: thread owns float4 column c4 (plane offset computed once) of
-    // rows tid / C4 + (256 / C4) * j
-    constexpr int C4 = NT * 4;
-    static_assert(256 % C4 == 0, "NT must divide 16");
-    const int col = 4 * (tid % C4);
-    if (col < hfp) {
-        const int g = col / slice_w;
-        float* dst = Wh + (size_t)g * (size_t)slice_stride + (col - g * slice_w);
-        const int rows = min(BM, n - blk0);
-        for (int r = tid / C4; r < rows; r += 256 / C4)
-            *reinterpret_cast<f32x4*>(dst + (size_t)(blk0 + r) * ld_wh) =
-                *reinterpret_cast<const f32x4*>(Os + r * OS + col);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Direct projection epilogue (the projection kernels' DIRECT form).  The MFMA
 // operands are swapped (A = W fragment, B = x fragment), so the accumulators
 // hold Wh^T: lane l (kq = l >> 4) has Wh[row][16t + 4kq .. +4] of its tile
@@ -470,16 +309,17 @@ __device__ __forceinline__ void proj_direct_epilogue(
 // large running sum at every step.
 //
 // Block: 64 rows x BN columns, one 16-row group per wave; 64-deep K chunks
-// through LDS as k_project_pipe2, but with TWO chunks' loads in flight (a
-// register double buffer): with the MFMA phase 2.7x shorter, one chunk in
-// flight left the loads exposed (the 128-row, one-ahead form of this kernel
-// ran Reddit in 196 us, 2.9 TB/s of x).
+// through LDS (as round 2's fp32-MFMA k_project_pipe2, removed in round 6:
+// 229-233 us at Reddit), with TWO chunks' loads in flight (a register double
+// buffer) where rows are 4-float aligned: with the MFMA phase 2.7x shorter,
+// one chunk in flight left the loads exposed (the 128-row, one-ahead form of
+// this kernel ran Reddit in 196 us, 2.9 TB/s of x).
 // x stays fp32 in LDS and each lane splits its own A fragment (8 consecutive k
 // of one row) after reading it — every x element is split exactly once; W is
 // split once per chunk at the LDS write, into three bf16 planes the waves
 // share.  Fragment maps (cdna_hip_programming.md §3): lane l holds
 // A[row l&15][k 8(l>>4)..+8] and B[k 8(l>>4)..+8][col l&15]; C/D as the fp32
-// form (col l&15, rows 4(l>>4)+i), so the epilogue is k_project_pipe2's.
+// form (col l&15, rows 4(l>>4)+i).
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -1211,178 +1051,6 @@ __global__ __launch_bounds__(256, 3) void k_project_wres_d(
     }
 }
 
-#ifdef GAT_AB_KERNELS  // measured and not adopted (profiles/r04/proj_ab.json); tools-only build
-// ---------------------------------------------------------------------------
-// Projection for fin in {32, 64, 128} (ogbn-arxiv's 128), split-bf16 MFMA:
-// W held in REGISTERS, x streamed through LDS by LDS-DMA.
-//
-// With K <= 128 and <= 64 columns, a lane's W fragments for every k-step and
-// column tile (split into three bf16 terms once, as k_project_x3 splits W)
-// are <= 16 x 3 bf16x8 = 192 VGPRs: each wave loads and splits them once and
-// then loops over 16-row x tiles with no W traffic at all (k_project_wres
-// re-reads 48 W fragments per tile from LDS).  A 16-row x tile is one
-// contiguous 16*fin*4-byte run (x 16-B aligned), fetched in whole 1-KiB
-// wave-instructions (global_load_lds_dwordx4, 8 per tile at fin = 128) into a
-// private ring of 4 LDS tile buffers: 3 tiles in flight while one is computed,
-// no VGPRs held by them and no per-element address arithmetic (fragment-shaped
-// loads touch 16 rows x 32 B per instruction).  The LDS image is XOR-swizzled
-// through the SOURCE address (LDS-DMA writes lane-linear): 16-B piece p of row
-// r lands at p ^ (r & 15), so the fragment reads (ds_read_b128, rows 0..15)
-// hit 16 distinct 4-bank groups.  Operands swapped as k_project_wk's DIRECT
-// form (A = W fragment, B = x fragment): each lane ends with four consecutive
-// Wh columns of one row, stored straight from registers (proj_direct_epilogue).
-// Ordering: a wave reads only ring buffers it filled, after a counted
-// s_waitcnt vmcnt that retires that tile's DMAs (the three younger tiles'
-// 3 * GLDS DMAs, and any younger stores, may stay in flight); a buffer is
-// refilled one tile after its fragments were read.  The DMAs are issued by
-// inline asm so that the compiler, which cannot see them, never adds a
-// conservative vmcnt(0) before the ring reads; its own waits for its own
-// loads can only be longer than needed, never shorter.
-// One workgroup of 4 waves per CU (one wave per SIMD: ~300 VGPRs).
-// ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-
-template <int NT, int KS, int EXTRA = 0>
-__global__ __launch_bounds__(256, 1) void k_project_wg(
-    const float* __restrict__ X, int n, int fin,
-    const float* __restrict__ W, const float* __restrict__ bW,
-    const float* __restrict__ a1, const float* __restrict__ c1,
-    const float* __restrict__ a2, const float* __restrict__ c2,
-    int H, int F, int HF, float* __restrict__ Wh, int ld_wh, float* __restrict__ Ss, int ld_s,
-    float* __restrict__ s_dst, int slice_w, long long slice_stride, int store_wt, int crows,
-    long long cjump) {
-    GAT_ROW_CHUNKS();
-    constexpr int BN = NT * 16, KP = KS * 32;  // fin == KP
-    constexpr int TILE = 16 * KP;              // floats per x tile
-    constexpr int PIECES = KP / 4;             // 16-B pieces per x row (8, 16 or 32)
-    constexpr int SWM = PIECES < 16 ? PIECES - 1 : 15;
-    constexpr int GLDS = TILE / 256;           // 1-KiB LDS-DMA wave-instructions per tile
-    static_assert(GLDS >= 1 && (PIECES & (PIECES - 1)) == 0, "fin must be 32, 64 or 128");
-    // four separate ring buffers (static references only)
-    __shared__ __attribute__((aligned(16))) float xr0[4][TILE];
-    __shared__ __attribute__((aligned(16))) float xr1[4][TILE];
-    __shared__ __attribute__((aligned(16))) float xr2[4][TILE];
-    __shared__ __attribute__((aligned(16))) float xr3[4][TILE];
-    __shared__ __attribute__((aligned(16))) float prm[3 * BN + 2 * 64];
-    float* bs = prm;
-    float* a1s = prm + BN;
-    float* a2s = prm + 2 * BN;
-    float* c1s = prm + 3 * BN;
-    float* c2s = c1s + 64;
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int cl = lane & 15, kq = lane >> 4;
-    const int tiles = (n + 15) / 16;
-    const int tstride = gridDim.x * 4;
-    int tile = blockIdx.x * 4 + w;
-    // this lane's source offsets inside a tile: DMA unit u = 64 i + lane holds
-    // row u / PIECES, stored piece u % PIECES = source piece ^ swizzle
-    int soff[GLDS], srow[GLDS];
-#pragma unroll
-    for (int i = 0; i < GLDS; ++i) {
-        const int u = i * 64 + lane;
-        srow[i] = u / PIECES;
-        soff[i] = 4 * ((u % PIECES) ^ (srow[i] & SWM));
-    }
-    auto fetch = [&](int tl, float* dst) {
-        const int t = min(tl, tiles - 1);  // past the end: a harmless reload
-        const bool full = t * 16 + 16 <= n;  // wave-uniform
-#pragma unroll
-        for (int i = 0; i < GLDS; ++i) {
-            const int grow = full ? t * 16 + srow[i] : min(t * 16 + srow[i], n - 1);
-            const float* src = X + (size_t)grow * KP + soff[i];
-            const unsigned ldst = __builtin_amdgcn_readfirstlane(
-                (unsigned)(uintptr_t)(lds_void_ptr)(dst + i * 256));  // wave-uniform
-            unsigned keep;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                : "=&s"(keep)
-                : "v"(src), "s"(ldst)
-                : "memory");
-        }
-    };
-    fetch(tile, xr0[w]);
-    fetch(tile + tstride, xr1[w]);
-    fetch(tile + 2 * tstride, xr2[w]);
-    // this lane's W fragments, split into three bf16 terms (zero past HF)
-    bf16x8 wf1[KS][NT], wf2[KS][NT], wf3[KS][NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int cc = t * 16 + cl;
-        const float* wr = W + (size_t)min(cc, HF - 1) * KP + 8 * kq;
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            f32x4 lo = *reinterpret_cast<const f32x4*>(wr + 32 * s2);
-            f32x4 hi = *reinterpret_cast<const f32x4*>(wr + 32 * s2 + 4);
-            if (cc >= HF) lo = hi = f32x4{0.f, 0.f, 0.f, 0.f};
-            split3_x8(lo, hi, wf1[s2][t], wf2[s2][t], wf3[s2][t]);
-        }
-    }
-    if (tid < BN) {
-        const bool ok = tid < HF;
-        const int cc = ok ? tid : 0;
-        const float bv = bW[cc], av1 = a1[cc], av2 = a2[cc];
-        bs[tid] = ok ? bv : 0.f;
-        a1s[tid] = ok ? av1 : 0.f;
-        a2s[tid] = ok ? av2 : 0.f;
-    }
-    if (tid < H) {
-        const float v1 = c1[tid], v2 = c2[tid];
-        c1s[tid] = v1;
-        c2s[tid] = v2;
-    }
-    __syncthreads();
-
-    auto compute_tile = [&](const float* __restrict__ xb, int tl) {
-        f32x4 acc[NT], cor[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = cor[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-            const int p0 = 8 * s2 + 2 * kq;
-            const f32x4 lo = *reinterpret_cast<const f32x4*>(xb + cl * KP + 4 * (p0 ^ (cl & SWM)));
-            const f32x4 hi =
-                *reinterpret_cast<const f32x4*>(xb + cl * KP + 4 * ((p0 + 1) ^ (cl & SWM)));
-            bf16x8 x1, x2, x3;
-            split3_x8(lo, hi, x1, x2, x3);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[s2][t], x1, acc[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf2[s2][t], x1, cor[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[s2][t], x2, cor[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf3[s2][t], x1, cor[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf2[s2][t], x2, cor[t], 0, 0, 0);
-                cor[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf1[s2][t], x3, cor[t], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[t][i] = split_sum(acc[t][i], cor[t][i]);
-        proj_direct_epilogue<NT>(acc, tl * 16 + cl, n, kq, bs, a1s, a2s, c1s, c2s, H, F, HF,
-                                 Wh, ld_wh, Ss, ld_s, s_dst, slice_w, slice_stride, store_wt);
-    };
-    // the ring, unrolled four ways so every buffer reference is static
-    auto step = [&](const float* cur, float* refill) -> bool {
-        if (tile >= tiles) return false;
-        fetch(tile + 3 * tstride, refill);
-        // this tile's DMAs retired; the next three tiles' (3 GLDS, issued
-        // later) may still fly.  Younger stores only make the wait longer.
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * GLDS + EXTRA) : "memory");
-        compute_tile(cur, tile);
-        tile += tstride;
-        return true;
-    };
-    while (step(xr0[w], xr3[w]) && step(xr1[w], xr0[w]) && step(xr2[w], xr1[w]) &&
-           step(xr3[w], xr2[w])) {
-    }
-    // the prefetches past the last tile must land before the workgroup's LDS is
-    // released (an LDS-DMA into a freed allocation would corrupt the next one)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-#endif  // GAT_AB_KERNELS
 
 // ---------------------------------------------------------------------------
 // Projection, whole-K variant (fin <= 64): the workgroup's 64 X rows are one
@@ -1622,111 +1290,53 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((nr + 63) / 64, ny), block(256);
     const int nt = (hf + 15) / 16;
-    const int store_wt = store_wt_on();  // Wh / scores stored write-through
-    // GAT_PROJ_KERNEL (A/B knob, tools/tests): "wk" (whole K in LDS; the
-    // default for fin <= 64), "pipe" (pipelined K loop; the default for larger
-    // fin), "tiled" / "lds" (K-tiled fallback, shuffle / LDS epilogue)
-    const char* pk = sliced ? nullptr : knob("GAT_PROJ_KERNEL");
+    const int store_wt = 1;  // Wh / scores stored write-through (sc1)
     const bool pow2_f = next_pow2(f) == f;
     const size_t wk_lds = (size_t)wk_lds_floats(fin, nt) * sizeof(float);
     const bool aligned16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) |
                              reinterpret_cast<uintptr_t>(wh)) & 15) == 0;
+    // x and W read LW floats at a time where fin and the pointers allow
+    const uintptr_t xwa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
+    const int lw = (fin % 4 == 0 && (xwa & 15) == 0) ? 4 : (fin % 2 == 0 && (xwa & 7) == 0) ? 2 : 1;
     // W-resident kernel for 64 < fin <= 128 (k_project_wres: arxiv 44.4 -> 38.4 us
     // against k_project_x3; at PPI's fin 50 the whole-K fp32 k_project_wk stays
-    // faster, 10.4 vs 12.5 us: 1.4 tiles per wave do not amortise the W split).
-    // GAT_PROJ_WRES (A/B knob): 0 never, 1 for every fin <= 128.
-    bool wres = fin > 64;
-    if (const char* v = knob("GAT_PROJ_WRES")) wres = std::atoi(v) != 0;
-    if (pk != nullptr && std::strcmp(pk, "wres") != 0) wres = false;
-    if (wres && fin > 0 && fin <= 128 && (nt == 1 || nt == 2 || nt == 4) && pow2_f && f <= 16) {
-        // x and W are both read LW floats at a time
-        const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
-        const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
-        const int ks = fin <= 32 ? 1 : fin <= 64 ? 2 : 4;
+    // faster, 10.4 vs 12.5 us: 1.4 tiles per wave do not amortise the W split)
+    if (fin > 64 && fin <= 128 && (nt == 1 || nt == 2 || nt == 4) && pow2_f && f <= 16) {
         const long long tiles = (nr + 15) / 16;
-        // persistent beyond the workgroups one CU holds at once (each wave loops
-        // over tiles): 3 per CU for K <= 64 (45 KB of LDS, <= 168 VGPRs), else 2
-        int wg_cu = ks <= 2 ? 3 : 2;
-        if (const char* v = knob("GAT_PROJ_WRES_WGS")) wg_cu = std::max(1, std::atoi(v));
-#ifdef GAT_AB_KERNELS
-        // GAT_PROJ_WG (A/B knob): k_project_wg (x through LDS by LDS-DMA) for fin
-        // in {32, 64, 128} with 16-B aligned x and heads of 4, 8 or 16 columns;
-        // "2": the same with a store-aware DMA wait (vmcnt + 10, A/B only)
-        int wg = 0;
-        if (const char* v = knob("GAT_PROJ_WG")) wg = std::atoi(v);
-        const bool wg_ok = (fin == 32 || fin == 64 || fin == 128) &&
-                           ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w)) & 15) == 0 &&
-                           (f == 4 || f == 8 || f == 16);
-        if (wg && wg_ok) {
-            const int grid_g = (int)std::max<long long>(1, std::min<long long>((tiles + 3) / 4, 256LL / ny));
-#define GAT_WG(NTV, KSV, EX)                                                                     \
-    hipLaunchKernelGGL((k_project_wg<NTV, KSV, EX>), dim3(grid_g, ny), dim3(256), 0, st, x, n, fin, \
-                       w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s,    \
-                       s_dst, slice_w, slice_stride, store_wt, crows, cjump)
-#define GAT_WG_KS(NTV, EX)                                  \
-    switch (ks) {                                           \
-        case 1: GAT_WG(NTV, 1, EX); break;                  \
-        case 2: GAT_WG(NTV, 2, EX); break;                  \
-        default: GAT_WG(NTV, 4, EX); break;                 \
-    }
-            if (wg == 2 && nt == 4) { GAT_WG_KS(4, 10) }
-            else if (nt == 1) { GAT_WG_KS(1, 0) }
-            else if (nt == 2) { GAT_WG_KS(2, 0) }
-            else { GAT_WG_KS(4, 0) }
-#undef GAT_WG_KS
-#undef GAT_WG
-            return status_of(hipGetLastError());
-        }
-#endif
         // the direct-epilogue form (heads of 4, 8 or 16 columns), three
         // workgroups per CU: arxiv 40.3 -> 31.7 us, a P = 8 rank's 21k rows
-        // 11.4 -> 9.9 us, same box (profiles/r05/proj_wres_direct.json).
-        // GAT_PROJ_WRES_DIRECT=0 (A/B knob): k_project_wres
-        bool wdir = true;
-        if (const char* v = knob("GAT_PROJ_WRES_DIRECT")) wdir = std::atoi(v) != 0;
-        wdir = wdir && (f == 4 || f == 8 || f == 16);
-        if (wdir) wg_cu = 3;
+        // 11.4 -> 9.9 us, same box (profiles/r05/proj_wres_direct.json);
+        // k_project_wres (output tile in LDS, two per CU) for heads of 1 or 2
+        const bool wdir = f == 4 || f == 8 || f == 16;
+        const int wg_cu = wdir ? 3 : 2;
         const int grid_w = (int)std::max<long long>(
             1, std::min<long long>((tiles + 3) / 4, 256LL * wg_cu / ny));
-#define GAT_WRES(NTV, LWV, KSV)                                                               \
-    if (wdir)                                                                                 \
-        hipLaunchKernelGGL((k_project_wres_d<NTV, LWV, KSV>), dim3(grid_w, ny), dim3(256), 0, \
+#define GAT_WRES(NTV, LWV)                                                                  \
+    if (wdir)                                                                               \
+        hipLaunchKernelGGL((k_project_wres_d<NTV, LWV, 4>), dim3(grid_w, ny), dim3(256), 0, \
                            st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, \
                            ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, \
-                           cjump);                                                            \
-    else                                                                                      \
-        hipLaunchKernelGGL((k_project_wres<NTV, LWV, KSV>), dim3(grid_w, ny), dim3(256), 0,   \
+                           cjump);                                                          \
+    else                                                                                    \
+        hipLaunchKernelGGL((k_project_wres<NTV, LWV, 4>), dim3(grid_w, ny), dim3(256), 0,   \
                            st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, \
                            ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, \
                            cjump)
-#define GAT_WRES_KS(NTV, LWV)                                          \
-    switch (ks) {                                                      \
-        case 1: GAT_WRES(NTV, LWV, 1); break;                          \
-        case 2: GAT_WRES(NTV, LWV, 2); break;                          \
-        default: GAT_WRES(NTV, LWV, 4); break;                         \
-    }
 #define GAT_WRES_LW(NTV)                                               \
-    if (lw == 4) { GAT_WRES_KS(NTV, 4) }                               \
-    else if (lw == 2) { GAT_WRES_KS(NTV, 2) }                          \
-    else { GAT_WRES_KS(NTV, 1) }
+    if (lw == 4) { GAT_WRES(NTV, 4); }                                 \
+    else if (lw == 2) { GAT_WRES(NTV, 2); }                            \
+    else { GAT_WRES(NTV, 1); }
         if (nt == 1) { GAT_WRES_LW(1) }
         else if (nt == 2) { GAT_WRES_LW(2) }
         else { GAT_WRES_LW(4) }
 #undef GAT_WRES_LW
-#undef GAT_WRES_KS
 #undef GAT_WRES
         return status_of(hipGetLastError());
     }
-    int wk_max = 64;  // GAT_PROJ_WK_MAX (A/B knob): largest fin for the whole-K kernel
-    // (at most 64: its staging loads cover 64 x 64 floats of X and W)
-    if (const char* v = knob("GAT_PROJ_WK_MAX")) wk_max = std::min(std::atoi(v), 64);
-    const bool wk_ok = fin > 0 && fin <= wk_max && aligned16 && wk_lds <= 160 * 1024 &&
-                       (pk == nullptr || std::strcmp(pk, "wk") == 0);
-    if (wk_ok) {
-        // the direct epilogue for heads of 4, 8 or 16 columns (GAT_PROJ_WK_DIRECT=0:
-        // the LDS output tile, A/B knob)
-        bool direct = f == 4 || f == 8 || f == 16;
-        if (const char* v = knob("GAT_PROJ_WK_DIRECT")) direct = direct && std::atoi(v) != 0;
+    // whole K in LDS (fin <= 64: its staging loads cover 64 x 64 floats of X and W)
+    if (fin > 0 && fin <= 64 && aligned16 && wk_lds <= 160 * 1024) {
+        // the direct epilogue for heads of 4, 8 or 16 columns
+        const bool direct = f == 4 || f == 8 || f == 16;
 #define GAT_WK_CASE(NT)                                                                       \
     case NT:                                                                                  \
         if (direct)                                                                           \
@@ -1749,117 +1359,55 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #undef GAT_WK_CASE
         return status_of(hipGetLastError());
     }
-    // pipelined K loop for large fin (F a power of two dividing 16, HF in
-    // {16, 32, 64}, i.e. nt in {1, 2, 4}); LW floats per lane where fin allows
-    const bool force_pipe = pk != nullptr && std::strcmp(pk, "pipe") == 0;
-    const bool pipe_ok = (fin > 64 || force_pipe) && fin > 0 &&
-                         (nt == 1 || nt == 2 || nt == 4) && pow2_f && f <= 16 &&
-                         (long long)n * fin < (1LL << 31) && (pk == nullptr || force_pipe);
-    if (pipe_ok) {
-        const dim3 gp((nr + 127) / 128, ny), bp(256);
-        const uintptr_t xa = reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w);
-        const int lw = (fin % 4 == 0 && (xa & 15) == 0) ? 4 : (fin % 2 == 0 && (xa & 7) == 0) ? 2 : 1;
-        // split-bf16 matrix cores (k_project_x3) unless GAT_PROJ_X3=0 (A/B knob:
-        // the fp32-MFMA k_project_pipe2)
-        bool x3 = true;
-#ifdef GAT_AB_KERNELS
-        if (const char* v = knob("GAT_PROJ_X3")) x3 = std::atoi(v) != 0;
-#endif
-        if (!x3 && ny > 1) return GAT_EUNSUPPORTED;  // k_project_pipe2 has no row chunks
-        // rows per block (GAT_PROJ_BM A/B knob: 64 = one 16-row group per wave,
-        // 128 = two, sharing every B fragment)
-        // tools/proj_ab.py: 4-float x rows (arxiv) prefer 64 rows per block with two
-        // chunks in flight, 2-float rows (Reddit's 602) 128 rows sharing B
-        // fragments with one chunk in flight
-        int bm = lw == 4 ? 64 : 128;
-        if (const char* v = knob("GAT_PROJ_BM")) bm = std::atoi(v);
-        // GAT_PROJ_X3V (A/B knob): block shape and register bound of k_project_x3.
-        // "b64p1": 64 rows, one chunk in flight; "b64p1w3": the same bounded to 3
-        // workgroups per CU; "b128w2": 128 rows bounded to 2 workgroups per CU
-        // (k_project_x3<.., 2, 1> unbounded takes 308 registers: one wave per SIMD)
-        // default for 8-B aligned rows (Reddit's 602): 64-row blocks, one chunk in
-        // flight (188 registers, 2 waves per SIMD; tools/proj_bench.py: full
-        // Reddit 204 -> 201 us, a P = 8 rank's 29k rows 34.4 -> 29.1 us: twice
-        // the blocks fill the CUs; profiles/r04/proj_ab.json)
-        int x3v = lw == 2 ? 1 : 0;
-        if (const char* v = knob("GAT_PROJ_X3V")) {
-            x3v = 0;
-            if (std::strcmp(v, "b64p1") == 0) x3v = 1;
-            else if (std::strcmp(v, "b64p1w3") == 0) x3v = 2;
-            else if (std::strcmp(v, "b128w2") == 0) x3v = 3;
-            else if (std::strcmp(v, "b64w2") == 0) x3v = 4;
-        }
-#ifdef GAT_AB_KERNELS
-#define GAT_PIPE2_FP32(NT, LWV)                                                                \
-        hipLaunchKernelGGL((k_project_pipe2<NT, LWV>), gp, bp, 0, st, x, n, fin, w, b, a_src, \
-                           c_src, a_dst, c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst,  \
-                           slice_w, slice_stride)
-#else
-#define GAT_PIPE2_FP32(NT, LWV) (void)gp
-#endif
-        // W pre-split once per call into the caller's workspace (gat_project_ex):
-        // the x3 form then stages bf16 W tiles without splitting them (the
-        // default when a workspace is given; GAT_PROJ_PRESPLIT=0 is the A/B knob
-        // back to the per-workgroup split).  Reddit 200 -> 190 us, same box
-        // (profiles/r05/proj_presplit_ab.json); equal at a P = 8 rank's 29k rows
+    // split-bf16 matrix cores, K-chunked, for large fin (F a power of two
+    // dividing 16, HF in {16, 32, 64}, i.e. nt in {1, 2, 4}):
+    //   * 4-float x rows (arxiv-like): 64-row blocks, two chunks in flight;
+    //   * 2-float rows (Reddit's 602): 64-row blocks, one chunk in flight
+    //     (tools/proj_bench.py: Reddit 204 -> 201 us, a P = 8 rank's 29k rows
+    //     34.4 -> 29.1 us: twice the blocks fill the CUs; profiles/r04/proj_ab.json;
+    //     re-measured against the other block shapes in round 5: 190.9 vs
+    //     207-242 us, profiles/r05/proj_x3v_reddit.json), on W pre-split once
+    //     per call into bf16 planes (k_split_w) when the caller passes the
+    //     workspace (gat_project_ex): Reddit 200 -> 190 us, same box
+    //     (profiles/r05/proj_presplit_ab.json);
+    //   * 1-float rows: 128-row blocks sharing every B fragment, one chunk.
+    if (fin > 64 && (nt == 1 || nt == 2 || nt == 4) && pow2_f && f <= 16 &&
+        (long long)n * fin < (1LL << 31)) {
+        const dim3 bp(256);
         const size_t need = wsplit_bytes(hf, fin);
-        bool presplit = x3 && ws != nullptr && need > 0 && ws_bytes >= need && x3v == 1 &&
-                        (reinterpret_cast<uintptr_t>(ws) & 15) == 0;
-        {
-            const char* v = knob("GAT_PROJ_PRESPLIT");
-            presplit = presplit && (v == nullptr || std::atoi(v) != 0);
-        }
+        const bool presplit = lw == 2 && (nt == 2 || nt == 4) && ws != nullptr && need > 0 &&
+                              ws_bytes >= need && (reinterpret_cast<uintptr_t>(ws) & 15) == 0;
         if (presplit) {
             const int bn = nt * 16, kpad = (fin + 63) / 64 * 64;
             const int units = bn * (kpad / 8);
             hipLaunchKernelGGL(k_split_w, dim3((units + 255) / 256), dim3(256), 0, st, w, hf, fin, bn,
                                kpad, reinterpret_cast<__bf16*>(ws));
         }
-#define GAT_X3V(NT, LWV, RGV, PDV, MB, BMV)                                                   \
+#define GAT_X3(NT, LWV, RGV, PDV, MB, BMV)                                                    \
     hipLaunchKernelGGL((k_project_x3<NT, LWV, RGV, PDV, MB>), dim3((nr + BMV - 1) / BMV, ny), bp, \
                        0, st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,   \
                        ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows,     \
                        cjump)
-#define GAT_X3PS(NT, LWV)                                                                      \
-    launch_x3_presplit<NT, LWV>(dim3((nr + 63) / 64, ny), bp, st, x, n, fin,                    \
-                                reinterpret_cast<const float*>(ws), b, a_src, c_src, a_dst, c_dst, \
-                                heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst, slice_w,           \
-                                slice_stride, store_wt, crows, cjump)
-#define GAT_PIPE2(NT, LWV)                                                                     \
-    if (x3 && presplit && (NT == 2 || NT == 4)) GAT_X3PS(NT, LWV);                             \
-    else if (x3 && x3v == 1) GAT_X3V(NT, LWV, 1, 1, 1, 64);                                    \
-    else if (x3 && x3v == 2) GAT_X3V(NT, LWV, 1, 1, 3, 64);                                    \
-    else if (x3 && x3v == 3) GAT_X3V(NT, LWV, 2, 1, 2, 128);                                   \
-    else if (x3 && x3v == 4) GAT_X3V(NT, LWV, 1, 2, 2, 64);                                    \
-    else if (x3 && bm == 128)                                                                  \
-        hipLaunchKernelGGL((k_project_x3<NT, LWV, 2, 1>), dim3((nr + 127) / 128, ny), bp, 0,   \
-                           st, x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh, \
-                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, \
-                           cjump);                                                            \
-    else if (x3)                                                                               \
-        hipLaunchKernelGGL((k_project_x3<NT, LWV, 1, 2>), dim3((nr + 63) / 64, ny), bp, 0, st,  \
-                           x, n, fin, w, b, a_src, c_src, a_dst, c_dst, heads, f, hf, wh,     \
-                           ld_wh, s_src, ld_s, s_dst, slice_w, slice_stride, store_wt, crows, \
-                           cjump);                                                            \
-    else                                                                                       \
-        GAT_PIPE2_FP32(NT, LWV)
-#define GAT_PIPE2_LW(NT)                                  \
-    if (lw == 4) { GAT_PIPE2(NT, 4); }                    \
-    else if (lw == 2) { GAT_PIPE2(NT, 2); }               \
-    else { GAT_PIPE2(NT, 1); }
-        if (nt == 1) { GAT_PIPE2_LW(1) }
-        else if (nt == 2) { GAT_PIPE2_LW(2) }
-        else { GAT_PIPE2_LW(4) }
-#undef GAT_PIPE2_LW
-#undef GAT_PIPE2
-#undef GAT_PIPE2_FP32
-#undef GAT_X3V
-#undef GAT_X3PS
+#define GAT_X3_NT(NT)                                                                          \
+    if (lw == 4) { GAT_X3(NT, 4, 1, 2, 1, 64); }                                               \
+    else if (lw == 2 && presplit)                                                              \
+        launch_x3_presplit<NT, 2>(dim3((nr + 63) / 64, ny), bp, st, x, n, fin,                 \
+                                  reinterpret_cast<const float*>(ws), b, a_src, c_src, a_dst,  \
+                                  c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst, slice_w, \
+                                  slice_stride, store_wt, crows, cjump);                       \
+    else if (lw == 2) { GAT_X3(NT, 2, 1, 1, 1, 64); }                                          \
+    else { GAT_X3(NT, 1, 2, 1, 1, 128); }
+        if (nt == 1) { GAT_X3_NT(1) }
+        else if (nt == 2) { GAT_X3_NT(2) }
+        else { GAT_X3_NT(4) }
+#undef GAT_X3_NT
+#undef GAT_X3
         return status_of(hipGetLastError());
     }
     if (sliced || ny > 1) return GAT_EUNSUPPORTED;  // the kernels below: row-major Wh, no chunks
-    const bool shfl = ((f <= 16 && 16 % f == 0) || (f % 16 == 0)) &&
-                      !(pk != nullptr && std::strcmp(pk, "lds") == 0);
+    // K-tiled fallback (unaligned x or W, other head widths): a shuffle
+    // epilogue where F divides 16 or is a multiple of 16, else an LDS one
+    const bool shfl = (f <= 16 && 16 % f == 0) || (f % 16 == 0);
 #define GAT_PROJ_CASE(NT)                                                                   \
     case NT:                                                                                \
         if (shfl)                                                                           \

@@ -707,9 +707,14 @@ def _sharded_workload(w, dev, world: int, rank: int, exchanger, args, strategies
             ms1 = (time.perf_counter() - t0) * 1e3 / args.steps
             ref = one().cpu()
             res["one_gpu"] = {"value": csr.num_edges / (ms1 * 1e-3), "ms_per_step": ms1,
+                              "launch": "eager",
                               "what": "the same layer forward on the whole graph on rank 0's "
                                       "GPU alone (bench.py's single-GPU path: the layer "
                                       "module, eager)"}
+            if keep_for_graph:
+                # the same forward replayed from a captured graph: the one-GPU
+                # value a graph-replayed N-rank step is compared with
+                res["one_gpu"]["graph"] = _one_gpu_graph(one, csr.num_edges, args)
         dist.barrier()
         from .graph import csr_cache
         csr_cache.clear()  # the module's own CSR of ei (rank 0): not needed any more
@@ -792,6 +797,34 @@ def _sharded_workload(w, dev, world: int, rank: int, exchanger, args, strategies
     return res
 
 
+def _one_gpu_graph(one, e_prime: int, args) -> Dict:
+    """``one`` (the layer forward on the whole graph) replayed from a captured
+    graph, timed as the eager steps are (synchronize around K replays)."""
+    try:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                one()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            one()
+    except Exception as exc:  # noqa: BLE001 -- reported; the eager value stands
+        return {"ok": False, "error": f"{type(exc).__name__}: {exc}"[:300]}
+    for _ in range(max(3, args.warmup)):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.replay()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    del g
+    return {"ok": True, "value": e_prime / (ms * 1e-3), "ms_per_step": ms, "launch": "hipGraph"}
+
+
 def capture_steps(sh: "ShardedGAT", xl, steps: int = 2) -> "torch.cuda.CUDAGraph":
     """``steps`` consecutive sharded forwards (the two ping-pong node tables,
     the chunk all-gathers included) captured into ONE graph: a replay is
@@ -813,7 +846,8 @@ def capture_steps(sh: "ShardedGAT", xl, steps: int = 2) -> "torch.cuda.CUDAGraph
     return g
 
 
-def graph_trial(ctx, world: int, rank: int, args, w_name: str) -> Dict:
+def graph_trial(ctx, world: int, rank: int, args, w_name: str,
+                compute_only: bool = False) -> Dict:
     """The headline all-gather strategy replayed from a captured graph (two
     steps per replay; ``capture_steps``), timed as the eager steps are
     (barrier + synchronize around K steps, max over ranks) and checked
@@ -821,25 +855,43 @@ def graph_trial(ctx, world: int, rank: int, args, w_name: str) -> Dict:
     step is host-bound (the c10d + RCCL enqueue of the all-gather alone is
     ~20-30 us at one rank), which the graph removes.  Runs after every eager
     measurement: a capture that fails on any rank (the ranks agree over the
-    host group before any replay) is reported, and no graph is replayed."""
+    host group before any replay) is reported, and no graph is replayed.
+
+    compute_only (the one-GPU rehearsal, whose host-staged exchange copies
+    through host memory and cannot be captured): both ping-pong tables are
+    filled by eager steps with the exchange, and the graph holds each rank's
+    projection and edge passes only (the remote rows stay those of the eager
+    exchange: the inputs do not change).  The capture, the ranks' agreement
+    and the replay run as in the real step; the value is not a step's."""
     sh, xl, ref, e_prime, key = ctx
     per = 2
     ok, err = 1, None
+    saved = sh.exchanger
     try:
+        if compute_only:
+            for _ in range(per):  # both tables, with the exchange
+                sh.forward(xl)
+            torch.cuda.synchronize()
+            sh.exchanger = NoExchange()
         g = capture_steps(sh, xl, per)
     except Exception as exc:  # noqa: BLE001 -- reported, never replayed
         ok, err, g = 0, f"{type(exc).__name__}: {exc}"[:300], None
     flag = torch.tensor([ok], dtype=torch.int64)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # default group: gloo, on the host
     if int(flag.item()) == 0:
+        sh.exchanger = saved
         return {"ok": False, "error": err or "capture failed on another rank"}
     reps = max(1, args.steps // per)
     t = _time_steps(g.replay, max(1, args.warmup // per), reps)
     ms = t * 1e3 / (reps * per)
-    d = {"ok": True, "strategy": key, "launch": f"hipGraph ({per} steps per replay)",
+    launch = f"hipGraph ({per} steps per replay)"
+    if compute_only:
+        launch += ", compute only (exchange eager before capture: rehearsal)"
+    d = {"ok": True, "strategy": key, "launch": launch, "compute_only": compute_only,
          "value": e_prime / (ms * 1e-3), "ms_per_step": ms}
     g.replay()
     torch.cuda.synchronize()
+    sh.exchanger = saved
     full = gather_output(sh.out, sh.bounds)
     if rank == 0:
         diff = float((full - ref).abs().max())
@@ -922,34 +974,61 @@ def bench_distributed(args, metric: str):
     chunk_choices = [1, 2, 4] if world > 1 else [1, 2]
     strategies = [("allgather", k) for k in chunk_choices] + [("replicate", 1)]
     # graph-replayed steps for the small shapes, where a rank's eager step is
-    # host-bound (not with the host-staged rehearsal exchange: it copies
-    # through host memory)
-    graph_names = set() if share or getattr(args, "no_dist_graph", False) else \
+    # host-bound; the one-GPU rehearsal (host-staged exchange, not capturable)
+    # captures each rank's compute only, to exercise the capture agreement and
+    # the replay, and never reports it as the step
+    graph_names = set() if getattr(args, "no_dist_graph", False) else \
         {nm for nm in names if nm in ("ppi", "arxiv", "cifar")}
     work = {}
     for nm in names:
         work[nm] = _sharded_workload(WORKLOADS[nm], dev, world, rank, exchanger, args,
                                      strategies, force_exchange=force,
                                      keep_for_graph=nm in graph_names)
-    # after every eager measurement: a failed capture cannot disturb them
-    for nm in names:
+    # the eager results reach the detail file before any capture is attempted
+    if rank == 0:
+        from .benchline import write_detail
+        write_detail({"stage": "eager measurements, before any graph capture",
+                      "workloads": {k: {kk: vv for kk, vv in v.items() if kk != "_graph_ctx"}
+                                    for k, v in work.items()}},
+                     getattr(args, "detail_out", None))
+    for i, nm in enumerate(names):
         ctx = work[nm].pop("_graph_ctx", None)
         if ctx is None:
             continue
-        gt = graph_trial(ctx, world, rank, args, nm)
+        gt = graph_trial(ctx, world, rank, args, nm, compute_only=share)
         del ctx
         work[nm]["graph"] = gt
-        if gt.get("ok") and gt["value"] > work[nm]["value"]:
-            # the same strategy and work per step, launched from the graph
+        if not gt.get("ok"):
+            # no further capture after a failure: free the other trials' tables
+            for rest in names[i + 1:]:
+                work[rest].pop("_graph_ctx", None)
+            torch.cuda.empty_cache()
+            break
+        if rank == 0:
+            og = work[nm]["one_gpu"]
+            work[nm]["speedup_vs_one_gpu_eager"] = work[nm]["value"] / og["value"]
+            if og.get("graph", {}).get("ok"):
+                gt["speedup_vs_one_gpu_graph"] = gt["value"] / og["graph"]["value"]
+        if not share and gt["value"] > work[nm]["value"]:
+            # the same strategy and work per step, launched from the graph; the
+            # speed-up against the one-GPU forward launched the same way
             work[nm]["eager"] = {"value": work[nm]["value"],
                                  "ms_per_step": work[nm]["ms_per_step"]}
             work[nm]["value"], work[nm]["ms_per_step"] = gt["value"], gt["ms_per_step"]
             work[nm]["launch"] = gt["launch"]
             if rank == 0:
-                work[nm]["speedup_vs_one_gpu"] = gt["value"] / work[nm]["one_gpu"]["value"]
-        if not gt.get("ok"):
-            break  # no further capture after a failure
+                og = work[nm]["one_gpu"]
+                if og.get("graph", {}).get("ok"):
+                    work[nm]["speedup_vs_one_gpu"] = gt["speedup_vs_one_gpu_graph"]
+                    work[nm]["speedup_launch_mode"] = "hipGraph vs hipGraph"
+                else:  # no graphed one-GPU value: keep the like-for-like eager ratio
+                    work[nm]["speedup_vs_one_gpu"] = work[nm]["speedup_vs_one_gpu_eager"]
+                    work[nm]["speedup_launch_mode"] = "eager vs eager (one-GPU capture failed)"
         torch.cuda.empty_cache()
+    for nm in names:
+        work[nm].pop("_graph_ctx", None)
+        if rank == 0:
+            work[nm].setdefault("speedup_launch_mode", "eager vs eager")
     weak = None
     if not getattr(args, "no_weak", False):
         weak = _ppi_blocks_weak(WORKLOADS["ppi"], dev, world, rank, args)
@@ -981,6 +1060,7 @@ def bench_distributed(args, metric: str):
                        "exchange": xname, "launch": head.get("launch", "eager")},
             "one_gpu_same_workload": head.get("one_gpu"),
             "speedup_vs_one_gpu": head.get("speedup_vs_one_gpu"),
+            "speedup_launch_mode": head.get("speedup_launch_mode"),
             "replicate": head.pop("replicate", None),
             "workloads": {k: v for k, v in work.items() if k != names[0]},
             "headline_detail": head,

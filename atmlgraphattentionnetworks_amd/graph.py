@@ -104,7 +104,7 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int,
         # PyG's index_select raises on the same input (GAT.py:53 -> __lift__)
         raise ValueError(f"edge_index contains node ids outside [0, {num_nodes})")
     return CSRGraph(rowptr, col, num_nodes, E + num_nodes, order,
-                    hub_plan(rowptr, order, E + num_nodes, col=col),
+                    hub_plan(rowptr, order, E + num_nodes, col=col, max_degree=int(max_degree)),
                     locality_hint(rowptr, col, num_nodes), int(max_degree))
 
 
@@ -144,21 +144,20 @@ def hub_segment_len(num_edges: int) -> int:
 
 
 def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
-             seg_len: Optional[int] = None, col: Optional[torch.Tensor] = None
-             ) -> Optional[HubPlan]:
+             seg_len: Optional[int] = None, col: Optional[torch.Tensor] = None,
+             max_degree: Optional[int] = None) -> Optional[HubPlan]:
     """The split schedule for rows with more than 2 * seg_len in-edges, or
     None when there are none (every uniform BASELINE graph).  ``order`` is
-    the degree-descending row order, so the hubs are its first rows.
+    the degree-descending row order, so the hubs are its first rows;
+    ``max_degree`` (the longest row, when known) skips the count.
     GAT_HUB_SPLIT=0 disables splitting."""
     if tuning.get("GAT_HUB_SPLIT") == "0" or rowptr.numel() <= 1:
         return None
     seg = seg_len or hub_segment_len(num_edges)
+    thresh = 2 * seg
+    if max_degree is not None and max_degree <= thresh:
+        return None  # (the CSR build read its longest row already: no device sync)
     deg = (rowptr[1:] - rowptr[:-1]).to(torch.int64)
-    # A/B knobs: GAT_HUB_MIN (split rows past this many edges, >= seg; default
-    # 2 * seg) and GAT_HUB_BAL=1 (a hub's segments of equal length, not seg
-    # edges and a short tail)
-    hub_min = tuning.get("GAT_HUB_MIN")
-    thresh = 2 * seg if hub_min is None else max(seg, int(hub_min))
     n_hub = int((deg > thresh).sum())
     if n_hub == 0:
         return None
@@ -172,20 +171,22 @@ def hub_plan(rowptr: torch.Tensor, order: torch.Tensor, num_edges: int,
     vhub = torch.repeat_interleave(torch.arange(n_hub, device=rowptr.device), nseg)
     k = torch.arange(n_v, device=rowptr.device) - vptr[vhub]
     rp = rowptr.to(torch.int64)
-    slen = (hdeg + nseg - 1) // nseg if tuning.get("GAT_HUB_BAL") == "1" \
-        else torch.full_like(hdeg, seg)
+    # segments of seg edges and a short tail (equal-length segments per hub
+    # measured slower on power-law Reddit: 2.072 -> 2.409 ms,
+    # profiles/r05/edge_ab_hubshape_powerlaw.json)
+    slen = torch.full_like(hdeg, seg)
     vb = rp[hub_rows][vhub] + k * slen[vhub]
     ve = torch.minimum(vb + slen[vhub], rp[hub_rows + 1][vhub])
     rest = o[n_hub:]
     i32 = torch.int32
     vrow = hub_rows[vhub]
     slot = None
-    if tuning.get("GAT_HUB_ORDER") != "hub" and col is not None:
+    if col is not None:
         # segments by the first source id they gather (stable): the segments
         # running together then sweep the same part of the node table, as
         # equal-length whole rows do (ascending sources within every row).
         # Power-law Reddit edge kernel 2.289 -> 2.242 ms against the hub-by-hub
-        # order (GAT_HUB_ORDER=hub, the A/B knob); whole rows by ascending
+        # order (without col: segments hub by hub); whole rows by ascending
         # degree measured 3.26 ms and were dropped (profiles/r05/
         # edge_ab_hub_order_powerlaw.json)
         perm = torch.sort(col[vb].to(torch.int64), stable=True).indices

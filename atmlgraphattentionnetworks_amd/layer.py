@@ -209,8 +209,6 @@ def edge_aggregate(csr, table: NodeTable, s_dst: torch.Tensor, heads: int, f: in
     if out is None:
         out = torch.empty(rows, width, dtype=torch.float32, device=table.wh.device)
     order = getattr(csr, "order", None)
-    if order is not None and tuning.get("GAT_EDGE_ORDER") == "natural":  # A/B knob
-        order = None
     hint = csr.kernel_hint() if hasattr(csr, "kernel_hint") else \
         csr.num_edges // max(csr.num_nodes, 1)
     if table.slices > 1:
@@ -363,13 +361,10 @@ class ForwardPlan:
         self.bound = None  # (pp, bias, lib, project call, edge call) for run()
         # the s_src table: only the gathered-score edge kernels read it (score
         # activations other than LeakyReLU in [0, 1], heads whose F/4 is not a
-        # power of two, or GAT_EDGE_SCORE=gather); the fused kernels recompute
-        # s_src from the Wh row they gather, so the projection skips it (arxiv:
-        # 5.4 MB of stores).  GAT_PROJ_SS=1 (A/B knob): always write it.
-        self.need_ss = (not fused_score_ok(heads, f, negative_slope)
-                        or tuning.get("GAT_EDGE_SCORE") == "gather"
-                        or tuning.get("GAT_EDGE_KERNEL") == "generic"
-                        or tuning.get("GAT_PROJ_SS") == "1")
+        # power of two); the fused kernels recompute s_src from the Wh row they
+        # gather, so the projection skips it (arxiv: 5.4 MB of stores; layer
+        # 85.6 -> 81.3 us, profiles/r05/edge_ab_projss_arxiv.json)
+        self.need_ss = not fused_score_ok(heads, f, negative_slope)
 
     def built_for(self, csr) -> bool:
         """This plan was built for `csr` (and that graph is still alive)."""

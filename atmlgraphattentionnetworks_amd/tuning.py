@@ -1,4 +1,4 @@
-"""Kernel-choice knobs (A/B measurement in tools/ and the variant tests).
+"""Kernel-choice knobs (the variant tests and A/B measurement in tools/).
 
 The GAT_* environment variables are read ONCE, when this module is imported
 (and by the HIP library at its first launch), never per forward.  Tools and
@@ -12,10 +12,9 @@ from __future__ import annotations
 import os
 from typing import Dict, Optional
 
-# knobs read on the Python side of the boundary
-PY_KNOBS = ("GAT_WH_SLICES", "GAT_EDGE_ORDER", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_SCHED",
-            "GAT_HUB_ORDER", "GAT_EDGE_SCORE", "GAT_EDGE_KERNEL", "GAT_PROJ_SS",
-            "GAT_HUB_MIN", "GAT_HUB_BAL")
+# knobs read on the Python side of the boundary: the node table's column
+# planes, hub splitting and its segment length, the scheduled CSR copy
+PY_KNOBS = ("GAT_WH_SLICES", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_SCHED")
 
 _values: Dict[str, Optional[str]] = {}
 # bumped by every reload(): cached launch plans (layer.ForwardPlan) key on it,

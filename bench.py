@@ -285,6 +285,9 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
             run()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / steps
+        # the same step replayed from a captured graph (the one-GPU value that
+        # graph-replayed per-rank compute is compared with: like for like)
+        ms_graph = ms if graph else _graph_step_ms(step, warmup, steps)
 
         # the two phases alone, on the plan the layer's forward builds
         pp = layer.packed()
@@ -347,6 +350,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
         "workload": name, "N": n, "E_prime": e_prime, "Fin": w.in_channels, "H": w.heads,
         "F": w.out_channels, "concat": w.concat,
         "value": e_prime / (ms * 1e-3), "unit": "edges/s", "ms_per_step": ms, "launch": launch,
+        "ms_per_step_graph": ms_graph,
         "csr_build_once_ms": csr_ms, "csr_build_warm_ms": csr_warm_ms,
         "phases_in_step_ms": None if fused else in_step,
         "edge_kernel": {
@@ -359,6 +363,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
             "l2_request_bytes": l2b, "l2_GBps": l2b / es / 1e9,
             "l2_frac": l2b / es / 1e9 / L2_PEAK_GBS,
             "effective_gather_GBps": alg / es / 1e9,
+            "algorithmic_8d_bytes": alg,
             "hub_rows_split": 0 if csr.hubs is None else csr.hubs.n_hub,
         },
         "projection": ({"ms": 0.0, "kernel": "fused into the edge kernel (Fin <= 4)",
@@ -373,12 +378,39 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
     return res
 
 
+def _graph_step_ms(step, warmup: int, steps: int):
+    """ms per ``step`` replayed from a captured graph (None if capture fails)."""
+    try:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+    except Exception:  # noqa: BLE001  (the eager number stands alone)
+        return None
+    for _ in range(warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / steps
+
+
 def fused_small_fin(fin: int, plan) -> bool:
-    """Whether the layer's eval forward runs the fused small-Fin kernel:
-    gat_layer_forward (the cached plan over the scheduled CSR) with Fin <= 4,
-    unless GAT_EDGE_XPROJ=0 (gat_edge.hip)."""
-    return (0 < fin <= 4 and plan.sched is not None and not plan.split
-            and os.environ.get("GAT_EDGE_XPROJ", "1") != "0")
+    """Whether the layer's eval forward runs the fused small-Fin kernel: the
+    cached plan enqueues gat_layer_forward (over the scheduled CSR, no hub
+    split), and the library says that call fuses this shape
+    (gat_layer_forward_fuses, include/gat_amd.h)."""
+    from atmlgraphattentionnetworks_amd import _lib
+    if plan.sched is None or plan.split:
+        return False
+    return _lib.load().gat_layer_forward_fuses(plan.n, fin, plan.heads, plan.f, int(plan.concat),
+                                               plan.slope) == 1
 
 
 def pmc_child(names) -> None:
@@ -518,8 +550,14 @@ def _roofline(meas: dict, traffic: dict) -> dict:
     ek = meas["edge_kernel"]
     es = ek["ms"] * 1e-3
     fab = traffic.get("edge_fabric_bytes") if traffic else None
+    alg8d = ek["algorithmic_8d_bytes"]
     r = {"bound": "hbm", "achieved": ek["compulsory_GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": ek["hbm_frac"], "traffic": fab,
+         # SURVEY.md §8(d)'s no-reuse model beside it: every edge gathers its
+         # source's Wh row as if from HBM; > 1 means the rows are re-read from
+         # L2 / the Infinity Cache, so it is not an HBM fraction
+         "achieved_8d": alg8d / es / 1e9, "frac_8d": alg8d / es / 1e9 / HBM_PEAK_GBS,
+         "algorithmic_8d_bytes_per_launch": alg8d,
          "kernel": ek["kernel"], "kernel_ms": ek["ms"],
          "algorithmic_bytes_per_launch": ek["compulsory_bytes"],
          "algorithmic_model": "compulsory: col 4/edge + rowptr and row schedule 8/row + Wh "
@@ -629,7 +667,9 @@ def emulated_ranks(meas: dict, ranks, exchanges=("allgather",)) -> dict:
     alone on this GPU (distributed.emulate_rank_times), plus the bytes each
     rank would receive in the all-gather.  ``compute_only_speedup_bound`` =
     the one-GPU step / the slowest rank's compute: what P GPUs could reach if
-    the collective were free (it is not; the N > 1 lines measure it)."""
+    the collective were free (it is not; the N > 1 lines measure it).  Like
+    for like: the graph-replayed one-GPU step over the graph-replayed per-rank
+    compute, and (``_eager``) the eager step over the eager compute."""
     from atmlgraphattentionnetworks_amd.distributed import emulate_rank_times
     from atmlgraphattentionnetworks_amd.graph import get_csr
     x, ei, layer = meas["_inputs"]
@@ -642,7 +682,9 @@ def emulated_ranks(meas: dict, ranks, exchanges=("allgather",)) -> dict:
                 # "allgather_k1": one unsplit edge pass (the compute floor, no overlap)
                 kind, chunks = ("allgather", 1) if exch == "allgather_k1" else (exch, None)
                 r = emulate_rank_times(layer, csr, x, p, exchange=kind, chunks=chunks)
-                r["compute_only_speedup_bound"] = meas["ms_per_step"] / r["max_compute_ms"]
+                g1 = meas.get("ms_per_step_graph")
+                r["one_gpu_step_ms_graph"] = g1
+                r["compute_only_speedup_bound"] = None if not g1 else g1 / r["max_compute_ms"]
                 r["compute_only_speedup_bound_eager"] = \
                     meas["ms_per_step"] / r["max_compute_ms_eager"]
                 r["per_rank"] = [{k: (round(v, 5) if isinstance(v, float) else v)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 10
+#define GAT_ABI_VERSION 11
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -279,9 +279,10 @@ int gat_edge_merge_ex(const int* hub_rows, const int* seg_ptr, const int* seg_sl
  * call's status (GAT_EUNSUPPORTED from the projection launches nothing).
  * ABI 10: with 0 < fin <= 4 the projection is fused into the edge kernel (one
  * launch that gathers x rows and projects them in registers) wherever that
- * kernel takes the shape (heads*f of 32 or 64 in heads of 4 or 8 columns,
- * 4-8 edges per chunk); wh, s_src and s_dst are then scratch the call does
- * not write.  Results are the two-launch path's up to fp32 rounding.
+ * kernel takes the shape (heads*f of 32 or 64 in heads of 4 or 8 columns;
+ * gat_layer_forward_fuses says which); wh, s_src and s_dst are then scratch
+ * the call does not write.  Results are the two-launch path's up to fp32
+ * rounding.
  */
 int gat_layer_forward(const float* x, int n, int fin, const float* w, const float* b,
                       const float* a_src, const float* c_src, const float* a_dst,
@@ -289,6 +290,15 @@ int gat_layer_forward(const float* x, int n, int fin, const float* w, const floa
                       float* s_dst, const int* seg_begin, const int* seg_end, const int* col,
                       const int* row_order, int concat, float negative_slope, const float* bias,
                       float* out, int edges_per_row_hint, void* stream);
+
+/*
+ * gat_layer_forward_fuses (ABI 11): 1 when gat_layer_forward with these
+ * arguments launches the fused small-Fin kernel (one launch, no Wh table),
+ * 0 when it launches the projection and then the edge kernel.  A pure
+ * function of the shape (and the library's knob snapshot); launches nothing.
+ * For callers that account for the launches (the benchmark).
+ */
+int gat_layer_forward_fuses(int n, int fin, int heads, int f, int concat, float negative_slope);
 
 /* Workspace bytes gat_csr_build needs for (num_edges, num_nodes). */
 int gat_csr_workspace_size(long long num_edges, int num_nodes, size_t* bytes);

@@ -68,18 +68,15 @@ def _hub_case(n, e_uniform, hubs, fin, H, F, concat, seed):
                                         # threads (segment groups of 85 / 42 threads)
                                         (3, 8, True), (6, 4, False)])
 @pytest.mark.parametrize("slices", ["1", None])
-@pytest.mark.parametrize("merge", [None, "0"])
-def test_split_hubs_match_oracle(H, F, concat, slices, merge, monkeypatch):
+def test_split_hubs_match_oracle(H, F, concat, slices, monkeypatch):
     """GAT_HUB_SEG=64 splits every row above 128 in-edges (here: 5 hubs of
     300-5000 edges, and the long uniform rows are whole); planes (default
-    layout at >= 16 edges/row, concat) and row-major tables; the workgroup
-    merge (default) and the one-wave merge (GAT_EDGE_MERGE=0)."""
+    layout at >= 16 edges/row, concat) and row-major tables; the hub merge
+    spread over a workgroup (k_edge_merge_wg)."""
     from atmlgraphattentionnetworks_amd.graph import csr_cache, get_csr
     monkeypatch.setenv("GAT_HUB_SEG", "64")
     if slices is not None:
         monkeypatch.setenv("GAT_WH_SLICES", slices)
-    if merge is not None:
-        monkeypatch.setenv("GAT_EDGE_MERGE", merge)
     csr_cache.clear()
     x, ei, state = _hub_case(1500, 30000, [(3, 5000), (700, 1200), (9, 300), (1499, 129),
                                            (0, 2048)], 24, H, F, concat, seed=H * F)
@@ -96,30 +93,29 @@ def test_split_hubs_match_oracle(H, F, concat, slices, merge, monkeypatch):
 
 def test_hub_schedule_orders_bitwise(monkeypatch):
     """Hub segments scheduled by source range (the default: gat_edge_merge_ex's
-    seg_slot) and hub by hub (GAT_HUB_ORDER=hub): every segment computes as
-    before and the merge combines a hub's segments in the same order, so the
-    outputs are bitwise equal."""
-    from atmlgraphattentionnetworks_amd import tuning
-    from atmlgraphattentionnetworks_amd.graph import csr_cache, get_csr
+    seg_slot) and hub by hub (graph.hub_plan without col): every segment
+    computes as before and the merge combines a hub's segments in the same
+    order, so the outputs are bitwise equal."""
+    from atmlgraphattentionnetworks_amd.graph import csr_cache, get_csr, hub_plan
+    from atmlgraphattentionnetworks_amd.layer import gat_forward
     monkeypatch.setenv("GAT_HUB_SEG", "64")
     x, ei, state = _hub_case(1500, 30000, [(3, 5000), (700, 1200), (9, 300), (1499, 129),
                                            (0, 2048)], 24, 8, 8, True, seed=7)
     layer = _layer(state, 24, 8, 8, True)
-    outs = []
-    for env in ({"GAT_HUB_ORDER": "hub"}, {}):
-        monkeypatch.delenv("GAT_HUB_ORDER", raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        tuning.reload()
-        csr_cache.clear()
-        eid = ei.to(DEV)
-        csr = get_csr(eid, 1500)
-        assert csr.hubs is not None
-        assert (csr.hubs.seg_slot is None) == ("GAT_HUB_ORDER" in env)
-        with torch.no_grad():
-            outs.append(layer(x.to(DEV), eid).cpu())
+    csr_cache.clear()
+    eid = ei.to(DEV)
+    csr = get_csr(eid, 1500)
+    assert csr.hubs is not None and csr.hubs.seg_slot is not None
+    by_hub = csr._replace(hubs=hub_plan(csr.rowptr, csr.order, csr.num_edges, seg_len=64))
+    assert by_hub.hubs.seg_slot is None and by_hub.hubs.n_vrows == csr.hubs.n_vrows
+    pp, bias = layer.packed(), layer.bias.detach()
+    xd = x.to(DEV)
+    with torch.no_grad():
+        outs = [gat_forward(xd, c, pp, bias, 8, 8, True).cpu() for c in (by_hub, csr)]
+        via_layer = layer(xd, eid).cpu()
     csr_cache.clear()
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[1], via_layer)
     ref = gat_layer_forward_from_state(state, x, ei, 8, True)
     torch.testing.assert_close(outs[1], ref, atol=ATOL, rtol=RTOL)
 
@@ -157,19 +153,6 @@ def test_hub_row_of_120k_edges():
         csr_cache.clear()
     assert_at_least_reference_accuracy(out2, state, x, ei, 8, True)
     torch.testing.assert_close(out2, out, atol=ATOL, rtol=RTOL)
-    # the one-wave merge (GAT_EDGE_MERGE=0) sums the segments in another order
-    os.environ["GAT_EDGE_MERGE"] = "0"
-    try:
-        tuning.reload()
-        csr_cache.clear()
-        eid3 = ei.to(DEV)
-        with torch.no_grad():
-            out3 = layer(x.to(DEV), eid3).cpu()
-    finally:
-        del os.environ["GAT_EDGE_MERGE"]
-        tuning.reload()
-        csr_cache.clear()
-    torch.testing.assert_close(out3, out, atol=1e-6, rtol=1e-6)
 
 
 def test_reddit_powerlaw_sampled_rows():

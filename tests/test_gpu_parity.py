@@ -22,65 +22,43 @@ def dev():
     return torch.device("cuda", 0)
 
 
-# Every parity case runs on the default kernels AND on one representative of
-# each other kernel family the library can dispatch to (selected by its env
-# knobs): the product paths a shape or a graph can take, not every knob value.
+# Every parity case runs on the default kernels AND under each knob the library
+# keeps (atmlgraphattentionnetworks_amd/csrc/gat_abi.hip kKnobNames; tuning.PY_KNOBS):
+# each forces a product path that a shape or a graph size also reaches, so the
+# small cases cover the kernels the full-size graphs run.  The other kernel
+# families (projection per Fin and head width, the gathered-score and generic
+# edge kernels, odd lane groups) are reached by the shapes in CASES.
 VARIANTS = {
     "fast": {},
-    # edge kernel: chunk length by hint (U = 8, 16), two float4s per lane, the
-    # pipelined Reddit-scale kernel, the gathered-s_src form, the generic one
-    "u8": {"GAT_EDGE_U": "8"},
+    # one lane group per row (the full-size launches; row-batched ids where
+    # rows average >= 16 in-edges), and four
+    "split1": {"GAT_EDGE_SPLIT": "1"},
+    "split4": {"GAT_EDGE_SPLIT": "4"},
+    # edges per chunk 8 / 16, two float4s per lane, the pipelined long-row kernel
+    "u8": {"GAT_EDGE_U": "8", "GAT_EDGE_SPLIT": "1"},
     "u16": {"GAT_EDGE_U": "16"},
-    "v2_natural": {"GAT_EDGE_V": "2", "GAT_EDGE_ORDER": "natural"},
-    "pipe_u16_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
-    "pipe_u8_v2": {"GAT_EDGE_PIPE": "1", "GAT_EDGE_U": "8", "GAT_EDGE_V": "2"},
-    # the head's lane count read at run time instead of the HL-specialised kernels
-    "hl_runtime": {"GAT_EDGE_HL": "0"},
+    "u16_v2_pipe": {"GAT_EDGE_U": "16", "GAT_EDGE_V": "2"},
+    "u16_v2_nopipe": {"GAT_EDGE_U": "16", "GAT_EDGE_V": "2", "GAT_EDGE_PIPE": "0"},
+    "v2": {"GAT_EDGE_V": "2", "GAT_EDGE_SPLIT": "1"},
+    # short-row col values one chunk ahead instead of 8 chunks per load
+    "no_rowcol": {"GAT_EDGE_ROWCOL": "0", "GAT_EDGE_SPLIT": "1"},
     # Fin <= 4: projection and edge kernel as two launches instead of the fused
     # small-Fin kernel (the default through gat_layer_forward)
     "no_xproj": {"GAT_EDGE_XPROJ": "0"},
-    # short-row col values one chunk ahead instead of 8 chunks per load
-    "no_rowcol": {"GAT_EDGE_ROWCOL": "0"},
-    # the s_src table written although the fused edge kernels recompute it
-    "proj_ss": {"GAT_PROJ_SS": "1"},
-    "gather_score": {"GAT_EDGE_SCORE": "gather", "GAT_EDGE_SCHED": "0"},
-    "generic": {"GAT_EDGE_KERNEL": "generic", "GAT_PROJ_KERNEL": "lds", "GAT_EDGE_SCHED": "0"},
     # the CSR-order launch (short rows take the scheduled copy by default)
     "nosched": {"GAT_EDGE_SCHED": "0"},
-    # two lane groups per row (short rows, U = 4/8, V = 1): forced on, and off
-    # (small test graphs take it by default)
-    "split2": {"GAT_EDGE_SPLIT": "2"},
-    "split1": {"GAT_EDGE_SPLIT": "1"},
-    "split4": {"GAT_EDGE_SPLIT": "4"},
-    # projection: k_project_x3 for 64 < fin <= 128 (WRES=0), k_project_wres for
-    # every fin <= 128, the tiled fallback; plain stores instead of write-through
-    "proj_wk": {"GAT_PROJ_WRES": "0"},
-    "proj_wres": {"GAT_PROJ_WRES": "1"},
-    # k_project_wres with its output-tile epilogue instead of the direct one
-    # (the default for heads of 4, 8, 16 columns)
-    "proj_wres_tile": {"GAT_PROJ_WRES": "1", "GAT_PROJ_WRES_DIRECT": "0"},
-    "proj_tiled": {"GAT_PROJ_KERNEL": "tiled"},
-    "proj_wk_lds_epilogue": {"GAT_PROJ_WK_DIRECT": "0"},
-    "plain_stores": {"GAT_STORE_WT": "0"},
-    # Fin > 128: W pre-split once per launch into gat_project_ex's workspace is
-    # the default; the per-workgroup split (GAT_PROJ_PRESPLIT=0), also for the
-    # 64-row one-chunk x3 form with 4-float / 1-float rows
-    "proj_no_presplit": {"GAT_PROJ_PRESPLIT": "0"},
-    "proj_x3_b64p1": {"GAT_PROJ_X3V": "b64p1"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
 }
 
+KNOBS = ("GAT_EDGE_U", "GAT_EDGE_V", "GAT_EDGE_PIPE", "GAT_EDGE_SPLIT", "GAT_EDGE_ROWCOL",
+         "GAT_EDGE_XPROJ", "GAT_BWD_KINK", "GAT_BWD_SL", "GAT_BWD_KERNEL", "GAT_WH_SLICES",
+         "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_SCHED")
+
 
 @pytest.fixture(params=list(VARIANTS))
 def variant(request, monkeypatch):
-    for k in ("GAT_EDGE_KERNEL", "GAT_PROJ_KERNEL", "GAT_EDGE_U", "GAT_EDGE_SCORE", "GAT_EDGE_V",
-              "GAT_EDGE_ORDER", "GAT_WH_SLICES", "GAT_PROJ_WK_MAX", "GAT_EDGE_PIPE",
-              "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_PROJ_WRES", "GAT_STORE_WT", "GAT_EDGE_SCHED",
-              "GAT_PROJ_BM", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WK_DIRECT",
-              "GAT_EDGE_SPLIT", "GAT_PROJ_WG", "GAT_PROJ_X3V", "GAT_EDGE_LDSDMA",
-              "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT", "GAT_EDGE_XPROJ",
-              "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL", "GAT_PROJ_SS"):
+    for k in KNOBS:
         monkeypatch.delenv(k, raising=False)
     for k, v in VARIANTS[request.param].items():
         monkeypatch.setenv(k, v)
@@ -144,7 +122,7 @@ CASES = [
     # pre-split W (Fin > 128, HF 32 / 64): K tails, mean mode
     (500, 5000, 202, 4, 8, True, "uniform"),
     (321, 4000, 138, 8, 8, False, "uniform"),
-    # the K-chunked projections (Fin > 128; Fin > 64 with GAT_PROJ_WRES=0): K tails and
+    # the K-chunked projections (Fin > 128; Fin > 64 with heads of 1-16 columns, F a power of 2): K tails and
     # partial column tiles
     (400, 5000, 65, 4, 8, True, "uniform"),  # one-column tail chunk, NT = 2
     (400, 5000, 130, 2, 4, False, "uniform"),  # HF = 8, NT = 1
@@ -160,6 +138,19 @@ CASES = [
     (333, 4000, 32, 2, 8, False, "uniform"),
     (1500, 20000, 64, 2, 16, True, "uniform"),
     (60000, 200000, 128, 8, 8, True, "uniform"),
+    # k_project_wres with the LDS output tile (heads of 2 columns, 64 < Fin <= 128)
+    (300, 3000, 80, 32, 2, True, "uniform"),
+    # the K-tiled projection: Fin > 64 with heads of 7 (LDS epilogue) or HF = 128
+    # (8 column tiles: shuffle epilogue)
+    (300, 3000, 100, 5, 7, True, "uniform"),
+    (300, 3000, 100, 8, 16, True, "uniform"),
+    # the gathered-score edge kernel (a head's lanes not a power of two: F = 12, 24)
+    (400, 8000, 20, 4, 12, True, "uniform"),
+    (400, 8000, 20, 2, 24, True, "uniform"),
+    # rows of ~40 and ~150 in-edges: U = 8 and the pipelined U = 16, V = 2 kernel by default
+    (500, 20000, 40, 8, 8, True, "uniform"),
+    (400, 60000, 24, 8, 8, True, "uniform"),
+    (400, 60000, 24, 4, 16, True, "uniform"),
 ]
 
 
@@ -190,7 +181,7 @@ def test_rowcol_bitwise(n, e, fin, H, F, concat, kind, monkeypatch):
     from atmlgraphattentionnetworks_amd.graph import csr_cache
     x, ei, state = random_case(n, e, fin, H, F, concat, seed=n + fin, kind=kind)
     outs = []
-    for env in ({}, {"GAT_EDGE_ROWCOL": "0"}):
+    for env in ({}, {"GAT_EDGE_ROWCOL": "0"}, {"GAT_EDGE_ROWCOL": "2"}):
         monkeypatch.delenv("GAT_EDGE_ROWCOL", raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -199,6 +190,7 @@ def test_rowcol_bitwise(n, e, fin, H, F, concat, kind, monkeypatch):
         outs.append(run_layer(layer_from_state(state, fin, F, H, concat), x, ei))
     csr_cache.clear()
     assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])
     if kind == "uniform":  # (a 30k-200k-edge hub row: tests/test_gpu_hubs.py's bar)
         ref = gat_layer_forward_from_state(state, x, ei, H, concat)
         torch.testing.assert_close(outs[0], ref, atol=ATOL, rtol=RTOL)
@@ -355,6 +347,11 @@ def test_sliced_table_equals_row_major(slices, H, F, fin, monkeypatch):
     # one lane group per row in both layouts (the two-group split of small
     # launches applies to some lane-group widths only, and regroups the sums)
     monkeypatch.setenv("GAT_EDGE_SPLIT", "1")
+    # planes narrower than 16 columns run lane groups of 1-2 lanes, which the
+    # library instantiates at 8 edges per chunk only: the row-major run then
+    # takes 8 too (the same chunks, so still bit for bit)
+    if H * F // slices < 16:
+        monkeypatch.setenv("GAT_EDGE_U", "8")
     monkeypatch.setenv("GAT_WH_SLICES", str(slices))
     assert wh_slices(H, F, True, 0.2) == slices
     pp = layer.packed()
@@ -441,17 +438,17 @@ def test_sliced_default_with_unaligned_x_view():
     assert rc == _lib.GAT_EUNSUPPORTED
 
 
-@pytest.mark.parametrize("fin,heads,x3v", [(602, 8, None), (138, 4, None), (602, 8, "b64p1"),
-                                           (200, 8, "b64p1"), (201, 4, "b64p1"),
-                                           (602, 4, "b64p1w3")])
+@pytest.mark.parametrize("fin,heads", [(602, 8), (138, 4), (202, 8), (200, 8), (201, 4)])
 @pytest.mark.parametrize("chunks", [1, 3])
-def test_projection_presplit_bitwise(fin, heads, x3v, chunks, monkeypatch):
-    """gat_project_ex with its workspace and GAT_PROJ_PRESPLIT=1 (W split once
-    per launch, k_split_w) equals the per-workgroup split bitwise (the same
-    exact 3-term split), for
-    row-major and planes tables, one launch over row chunks included; without a
-    workspace, or one too small, it falls back to the per-workgroup split."""
-    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, _lib, tuning
+def test_projection_presplit_bitwise(fin, heads, chunks):
+    """gat_project_ex with its workspace (W split once per launch into bf16
+    planes, k_split_w: 2-float x rows, 2 or 4 column tiles) equals the
+    per-workgroup split bitwise (the same exact 3-term split), for row-major
+    and planes tables, one launch over row chunks included; without a
+    workspace, or with one too small, it takes the per-workgroup split.
+    4-float rows (200) and 1-float rows (201) never pre-split: all four calls
+    run the same kernel."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer, _lib
     from atmlgraphattentionnetworks_amd.layer import project_workspace
     d = dev()
     torch.manual_seed(1)
@@ -468,12 +465,7 @@ def test_projection_presplit_bitwise(fin, heads, x3v, chunks, monkeypatch):
             continue  # row chunks are a planes-table form
         crows = ((n + chunks - 1) // chunks + 63) // 64 * 64 if chunks > 1 else 0
         outs = []
-        for presplit, wsa in (("1", (ws.data_ptr(), ws.numel())), ("0", (ws.data_ptr(), ws.numel())),
-                              ("1", (0, 0)), ("1", (ws.data_ptr(), ws.numel() - 16))):
-            monkeypatch.setenv("GAT_PROJ_PRESPLIT", presplit)
-            if x3v:
-                monkeypatch.setenv("GAT_PROJ_X3V", x3v)
-            tuning.reload()
+        for wsa in ((ws.data_ptr(), ws.numel()), (0, 0), (ws.data_ptr(), ws.numel() - 16)):
             # row chunk c of ``crows`` rows goes to block c of (n rounded) rows
             blk = crows if crows else n
             nblk = (n + blk - 1) // blk
@@ -503,30 +495,37 @@ def test_projection_presplit_bitwise(fin, heads, x3v, chunks, monkeypatch):
                                        atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("fin,kernel", [(50, None), (50, "tiled"), (128, None), (100, None),
-                                        (200, None), (602, None), (130, "tiled"),
-                                        (128, "wres_tile"), (100, "wres_tile")])
-def test_projection_non_finite_inputs(fin, kernel, monkeypatch):
+@pytest.mark.parametrize("fin,H,F,unaligned", [
+    (50, 8, 8, False),    # k_project_wk (direct epilogue)
+    (50, 8, 8, True),     # k_project (K-tiled: x not 16-B aligned)
+    (128, 8, 8, False),   # k_project_wres_d
+    (100, 8, 8, False),
+    (200, 8, 8, False),   # k_project_x3, 4-float rows
+    (602, 8, 8, False),   # k_project_x3 on pre-split W
+    (130, 8, 8, True),    # K-tiled, Fin > 128
+    (128, 32, 2, False),  # k_project_wres (LDS output tile)
+    (100, 32, 2, False),
+], ids=["wk", "tiled50", "wres_d128", "wres_d100", "x3_200", "x3_602", "tiled130", "wres128",
+        "wres100"])
+def test_projection_non_finite_inputs(fin, H, F, unaligned):
     """Non-finite x (include/gat_amd.h, gat_project): rows without a
     non-finite value are unaffected (no leak into other rows through clamped
     or padded loads), and the rows with one equal the reference's fp32
     ``Linear`` (GAT.py:43-45) — +Inf, -Inf and NaN in the same places, for the
-    fp32-MFMA kernel (fin <= 64) and the split-bf16 ones (fin > 64), whose
-    correction products of an infinite x are dropped (split_sum)."""
+    fp32-MFMA kernels (fin <= 64, the K-tiled one) and the split-bf16 ones
+    (fin > 64), whose correction products of an infinite x are dropped
+    (split_sum)."""
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer
-    from atmlgraphattentionnetworks_amd import tuning
     from atmlgraphattentionnetworks_amd.layer import alloc_table, project
-    if kernel == "wres_tile":
-        monkeypatch.setenv("GAT_PROJ_WRES_DIRECT", "0")
-    elif kernel is not None:
-        monkeypatch.setenv("GAT_PROJ_KERNEL", kernel)
-    tuning.reload()
     d = dev()
     torch.manual_seed(0)
-    H, F, n = 8, 8, 700
+    n = 700
     layer = GraphAttentionLayer(fin, F, num_heads=H, concat=True).to(d).eval()
     x = torch.randn(n, fin, device=d)
     clean = x.clone()
+    if unaligned:  # views 4 bytes past a 256-B boundary: the library takes k_project
+        x = torch.empty(n * fin + 1, device=d)[1:].view(n, fin).copy_(x)
+        clean = torch.empty(n * fin + 1, device=d)[1:].view(n, fin).copy_(clean)
     bad_rows = [0, 17, 351, 500, n - 1]
     x[0, 3] = float("inf")
     x[17, fin - 1] = float("-inf")

@@ -180,10 +180,10 @@ def test_kink_sums_backward_equals_edge_pass(shape, p, monkeypatch):
 def test_source_pass_straight_line_bitwise(hfc, p, u, monkeypatch):
     """k_bwd_sources_sl (HF = 64 at 8 or 16 edges per chunk, GAT_BWD_SL=1) runs
     the same arithmetic in the same order as k_bwd_sources (GAT_BWD_SL=0):
-    every gradient bitwise equal, and both meet the float64 oracle."""
+    every gradient bitwise equal, and both meet the float64 oracle.  The chunk
+    length follows the edges per row (~45: 8, ~90: 16)."""
     H, F, concat = hfc
-    monkeypatch.setenv("GAT_BWD_U", u)
-    n, e, fin = 900, 14000, 40
+    n, e, fin = 900, {"8": 40000, "16": 80000}[u], 40
     layer, state, ei, x = _layer_and_ref(n, e, fin, H, F, concat, seed=21)
     seed = 0xBEEF
     drop = torch.from_numpy(dropout_factors(csr_positions(ei, n), H, p, seed)) if p else None

@@ -1,7 +1,8 @@
 """Host logic of the hub split (graph.hub_plan, CPU): the schedule the edge
 kernel walks and the segment-to-state map gat_edge_merge_ex reads.
 
-Invariants, for both segment orders (the default, and GAT_HUB_ORDER=hub):
+Invariants, for both segment orders (the default, and hub by hub when
+hub_plan is not given the CSR's col):
 - positions [0, n_vrows) are the hub segments, each covering seg_len in-edges
   of its hub (the last one the remainder), and together exactly the hub's row;
 - the positions after them are every other row once, whole;
@@ -9,7 +10,7 @@ Invariants, for both segment orders (the default, and GAT_HUB_ORDER=hub):
   runs at, so the merge combines a hub's segments in row order whatever the
   schedule (the bitwise-equality claim of tests/test_gpu_hubs.py);
 - default: hub segments sorted by the first source id they gather;
-  GAT_HUB_ORDER=hub: hub by hub, in row order (no seg_slot);
+  without col: hub by hub, in row order (no seg_slot);
 - whole rows by descending in-degree.
 """
 import numpy as np
@@ -38,19 +39,17 @@ def _csr(n, e, hubs, seed):
             torch.from_numpy(src.astype(np.int32)), deg)
 
 
-@pytest.mark.parametrize("env", [{}, {"GAT_HUB_ORDER": "hub"}])
-def test_hub_plan_invariants(env, monkeypatch):
+@pytest.mark.parametrize("by_src", [True, False])
+def test_hub_plan_invariants(by_src, monkeypatch):
     from atmlgraphattentionnetworks_amd import tuning
     from atmlgraphattentionnetworks_amd.graph import hub_plan
-    for k in ("GAT_HUB_ORDER", "GAT_HUB_SPLIT", "GAT_HUB_SEG"):
+    for k in ("GAT_HUB_SPLIT", "GAT_HUB_SEG"):
         monkeypatch.delenv(k, raising=False)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     tuning.reload()
     n = 3000
     rowptr, order, col, deg = _csr(n, 40000, [(5, 7000), (17, 2600), (2999, 1300), (0, 900)],
                                    seed=4)
-    plan = hub_plan(rowptr, order, int(rowptr[-1]), seg_len=256, col=col)
+    plan = hub_plan(rowptr, order, int(rowptr[-1]), seg_len=256, col=col if by_src else None)
     assert plan is not None and plan.seg_len == 256
     rp = rowptr.numpy().astype(np.int64)
     hub_rows = plan.hub_rows.numpy()
@@ -61,7 +60,6 @@ def test_hub_plan_invariants(env, monkeypatch):
     srow, sb, se = plan.sched_row.numpy(), plan.sched_b.numpy(), plan.sched_e.numpy()
     assert srow.size == nv + n - plan.n_hub
     slot = np.arange(nv) if plan.seg_slot is None else plan.seg_slot.numpy()
-    by_src = env.get("GAT_HUB_ORDER") != "hub"
     assert (plan.seg_slot is not None) == by_src
     assert sorted(slot.tolist()) == list(range(nv))  # a permutation of the segment positions
     for k, r in enumerate(hub_rows):
