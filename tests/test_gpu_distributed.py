@@ -234,6 +234,19 @@ def test_bench_two_ranks_shared_gpu(tmp_path):
     arx = d["workloads"]["arxiv"]
     assert arx["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * arx["check"]["max_abs_ref"]
     assert d["ppi_blocks_data_parallel"]["value"] > 0
+    # the graph path's control flow at world 2: each rank captured its compute
+    # (the host-staged exchange is not capturable), the ranks agreed, the
+    # replay ran and its gathered output matched the one-GPU forward; a
+    # rehearsal value never replaces the step's
+    for w in (head, arx):
+        g = w["graph"]
+        assert g["ok"] and g["compute_only"], g
+        assert g["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * g["check"]["max_abs_ref"]
+        assert w.get("launch", "eager") == "eager"
+    # the reported speed-up compares like with like
+    assert d["speedup_launch_mode"] == "eager vs eager"
+    assert d["one_gpu_same_workload"]["launch"] == "eager"
+    assert d["one_gpu_same_workload"]["graph"]["ok"]
 
 
 _RCCL_ONE_RANK = r"""
@@ -332,8 +345,15 @@ def test_bench_dist_one_rank_rccl(tmp_path):
     assert g["check"]["max_abs_diff_vs_one_gpu"] <= 1e-5 + 1e-5 * g["check"]["max_abs_ref"]
     # the headline is the faster launch of the same strategy
     assert d["value"] >= g["value"] * (1 - 1e-9)
-    if "eager" in head:  # the graph won
+    og = d["one_gpu_same_workload"]
+    assert og["launch"] == "eager" and og["graph"]["ok"]
+    if "eager" in head:  # the graph won: its speed-up is over the graphed one-GPU step
         assert d["value"] == g["value"] and d["config"]["launch"].startswith("hipGraph")
+        assert d["speedup_launch_mode"] == "hipGraph vs hipGraph"
+        assert abs(d["speedup_vs_one_gpu"] / (d["value"] / og["graph"]["value"]) - 1) < 1e-9
+    else:
+        assert d["speedup_launch_mode"] == "eager vs eager"
+        assert abs(d["speedup_vs_one_gpu"] / (d["value"] / og["value"]) - 1) < 1e-9
 
 
 def test_bench_single_gpu_line(tmp_path):
@@ -361,6 +381,8 @@ def test_bench_single_gpu_line(tmp_path):
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in roof, k
     assert 0 < roof["frac"] <= 1 and roof["unit"] == "GB/s"
+    # SURVEY §8(d)'s no-reuse model beside the compulsory one, from the same kernel time
+    assert roof["frac_8d"] > roof["frac"] and roof["achieved_8d"] > roof["achieved"]
     cb = line["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"]
     d = json.load(open(tmp_path / "detail.json"))

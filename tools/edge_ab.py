@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Interleaved A/B of edge-kernel variants in the layer's own table layout
 (sliced planes where the layer uses them), in ONE process.  A variant is a set
-of GAT_* knobs, e.g. ``base`` (no knobs) or ``GAT_EDGE_R=2,GAT_EDGE_U=8``.
+of GAT_* knobs, e.g. ``base`` (no knobs) or ``GAT_EDGE_U=8,GAT_EDGE_SPLIT=1``.
 Outputs are compared against the first variant (max |diff|).
 
     python tools/edge_ab.py --workload reddit --rounds 5 \
-        --variants "base;GAT_EDGE_R=2,GAT_EDGE_U=8;GAT_EDGE_R=4,GAT_EDGE_U=8"
+        --variants "base;GAT_EDGE_U=8;GAT_EDGE_PIPE=0"
 
 ``--only K`` runs variant K alone, ``--iters`` times, eagerly (for rocprofv3
 --pmc passes: every launch of the kernel is then that variant).
@@ -23,16 +23,10 @@ import torch  # noqa: E402
 
 from atmlgraphattentionnetworks_amd import tuning  # noqa: E402
 
-from tune_edge import time_fn  # noqa: E402
+from timing import time_fn  # noqa: E402
 
-KNOBS = ("GAT_EDGE_R", "GAT_EDGE_U", "GAT_EDGE_V", "GAT_EDGE_PIPE", "GAT_EDGE_LDS",
-         "GAT_WH_SLICES", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_ORDER", "GAT_PROJ_X3",
-         "GAT_PROJ_KERNEL", "GAT_PROJ_WK_MAX", "GAT_PROJ_BM",
-         "GAT_PROJ_WRES", "GAT_PROJ_WRES_WGS", "GAT_PROJ_WRES_NW", "GAT_STORE_WT",
-         "GAT_EDGE_SCHED", "GAT_EDGE_SPLIT", "GAT_EDGE_LDSDMA", "GAT_PROJ_WG", "GAT_PROJ_X3V",
-         "GAT_HUB_ORDER", "GAT_PROJ_PRESPLIT", "GAT_EDGE_HL", "GAT_PROJ_WRES_DIRECT",
-         "GAT_EDGE_XPROJ", "GAT_EDGE_MERGE", "GAT_EDGE_ROWCOL", "GAT_PROJ_SS", "GAT_EDGE_SCORE",
-         "GAT_HUB_MIN", "GAT_HUB_BAL")
+KNOBS = ("GAT_EDGE_U", "GAT_EDGE_V", "GAT_EDGE_PIPE", "GAT_EDGE_SPLIT", "GAT_EDGE_ROWCOL",
+         "GAT_EDGE_XPROJ", "GAT_WH_SLICES", "GAT_HUB_SPLIT", "GAT_HUB_SEG", "GAT_EDGE_SCHED")
 
 
 def parse(spec):

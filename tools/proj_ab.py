@@ -3,7 +3,7 @@
 ONE process, with each variant's error against a float64 torch restatement of
 Wh = x W^T + b and s_dst (GAT.py:42-52).  Variants are GAT_* knob sets.
 
-    python tools/proj_ab.py --workload arxiv --variants "GAT_PROJ_X3=0;base"
+    python tools/proj_ab.py --workload arxiv --variants "base"
 """
 import argparse
 import json
@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import torch  # noqa: E402
 
 from edge_ab import apply, parse  # noqa: E402
-from tune_edge import time_fn  # noqa: E402
+from timing import time_fn  # noqa: E402
 
 
 def main():
@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--workload", default="arxiv")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--variants", default="GAT_PROJ_X3=0;base")
+    ap.add_argument("--variants", default="base")
     args = ap.parse_args()
     from atmlgraphattentionnetworks_amd import GraphAttentionLayer, _lib, get_csr
     from atmlgraphattentionnetworks_amd.layer import ForwardPlan

@@ -9,7 +9,7 @@ ROWS rows (a rank's share of the partitioned step, e.g. reddit@29120 at P = 8).
 The table layout is the eval forward's (2 column planes at >= 16 edges/row).
 
     python tools/proj_bench.py --shapes "reddit,reddit@29120,arxiv,ppi" \
-        --variants "base;GAT_PROJ_BM=64" --out gpurun_out/proj_bench.json
+        --variants "base" --out gpurun_out/proj_bench.json
 """
 import argparse
 import json

@@ -5,7 +5,7 @@ them, so each kernel is timed in the cache state the step leaves it (the
 projection runs right after the previous step's edge kernel).  Variants are
 library env knobs, interleaved over rounds in one process.
 
-    python tools/step_probe.py --workload ppi --variants 'base:;dpp:GAT_PROJ_SCORES=dpp'
+    python tools/step_probe.py --workload ppi --variants 'base:;u8:GAT_EDGE_U=8'
 """
 import argparse
 import json

@@ -4,7 +4,7 @@
 The gradient cross-check is meaningful only with --dropout 0: the dropout
 seed comes from a device counter that torch.manual_seed does not reset.
 
-    python tools/train_ab.py --workload reddit --variants 'base:;lds:GAT_BWD_LDS=54000'
+    python tools/train_ab.py --workload reddit --variants 'base:;nokink:GAT_BWD_KINK=0'
 """
 import argparse
 import json
