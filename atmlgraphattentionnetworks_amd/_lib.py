@@ -20,6 +20,7 @@ GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
 GAT_ABI_VERSION = 11
 GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
+GAT_HINT_SHORT = 1 << 29  # every row < 1024 in-edges (include/gat_amd.h, ABI 11)
 GAT_SEG_LOAD = 1
 GAT_SEG_STORE = 2
 GAT_MAX_HEADS = 64

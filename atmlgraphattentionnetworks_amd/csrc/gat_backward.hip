@@ -1014,7 +1014,7 @@ int gat_bwd_table_layout(int heads, int f, int concat, int* ld_t) {
 
 // edges per chunk of the recompute backward kernels: the forward's thresholds
 static int bwd_unroll(int hint) {
-    hint &= ~GAT_HINT_LOCAL;
+    hint &= ~(GAT_HINT_LOCAL | GAT_HINT_SHORT);
     return hint <= 0 ? 8 : hint <= 32 ? 4 : hint <= 64 ? 8 : 16;
 }
 
@@ -1151,7 +1151,7 @@ int gat_bwd_sources(const int* csc_ptr, const int* csc_dst, const int* csc_eid, 
     // (profiles/r05/train_ab_sl_*.json)
     // (its id prefetch takes buffer loads of 31-bit byte offsets: E' < 2^29,
     // judged from the edges-per-row hint, floor(E'/N))
-    const long long hint = edges_per_row_hint & ~GAT_HINT_LOCAL;
+    const long long hint = edges_per_row_hint & ~(GAT_HINT_LOCAL | GAT_HINT_SHORT);
     bool sl = hf == 64 && (u == 8 || u == 16) && (f == 4 || f == 8 || f == 16) && hint > 0 &&
               (hint + 1) * (long long)num_nodes < (1LL << 29);
     {
@@ -1212,7 +1212,7 @@ int gat_edge_backward_rows(const int* rowptr, const int* col, const int* row_ord
                         kernel_choice("GAT_BWD_KERNEL", "generic");
     if (grp_ok) {
         const int g = next_pow2(hf / 4);
-        const int hint = edges_per_row_hint & ~GAT_HINT_LOCAL;
+        const int hint = edges_per_row_hint & ~(GAT_HINT_LOCAL | GAT_HINT_SHORT);
         const int u = hint > 0 && hint <= 12 ? 4 : 8;
         const long long threads = (long long)rows * g;
         const dim3 grid((unsigned)((threads + 255) / 256)), block(256);

@@ -236,8 +236,11 @@ struct XRow {  // one x row of the small-Fin form: N floats, 4-B aligned
 // was the walk's critical path at short rows (tools/edge_bisect.hip: a
 // memory-only PPI walk 24.4 -> 21.4 us).  Same chunks, ids and order:
 // results are bitwise the one-chunk-ahead form's.
+// LEAN (eval, rows < 1024 edges: GAT_HINT_SHORT): no Kahan sums and no dropout
+// code, so the registers they hold go to RC = 2's second chunk in flight.
+// RC = 2 (LEAN only): the row-batched ids AND the gathers one chunk ahead.
 template <int G, int U, int V, bool FUSED, bool PIPE = false, bool KINK = false, int S = 1,
-          int HL = 0, int XF = 0, int RC = 0>
+          int HL = 0, int XF = 0, int RC = 0, bool LEAN = false>
 __global__ __launch_bounds__(256) void k_edge_grp(
     const EdgeRows er, const int* __restrict__ col, const int* __restrict__ order,
     int row_begin, int row_end,
@@ -252,6 +255,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     static_assert(S == 1 || ((S == 2 || S == 4) && !KINK && !PIPE && G * S <= kWave), "split rows");
     static_assert(XF == 0 || (V == 1 && FUSED && !KINK && !PIPE && S == 1), "small-Fin form");
     static_assert(RC == 0 || (U == 4 && G >= 4 && S == 1 && !PIPE), "row-batched col values");
+    static_assert(!LEAN || (!KINK && XF == 0), "lean: the eval forward");
+    static_assert(RC != 2 || LEAN, "pipelined row-batched ids: lean only");
     // col values held per lane per chunk.  Groups of >= 4 lanes: every quad of
     // the group holds the chunk's indices (lane c: edges (c & 3) + 4t), so the
     // source ids are broadcast by DPP within the quad instead of LDS permutes
@@ -323,8 +328,8 @@ __global__ __launch_bounds__(256) void k_edge_grp(
     };
     const int si = er.by_pos ? pos : r;  // segment / state index
     const int e0 = er.eb[si], e1 = er.ee[si];
-    const bool kahan = e1 - e0 >= 1024;
-    const bool dropping = drop.thresh != 0u;  // kernel-uniform: a scalar branch
+    const bool kahan = !LEAN && e1 - e0 >= 1024;
+    const bool dropping = !LEAN && drop.thresh != 0u;  // kernel-uniform: a scalar branch
     // the target's share of every score, in log2 units (LeakyReLU is positively
     // homogeneous: LReLU(z) log2e = LReLU(z log2e)); + c1 when s_src is recomputed
     float sdv;
@@ -467,7 +472,9 @@ __global__ __launch_bounds__(256) void k_edge_grp(
                 kink(u, p, pa, racc, accq);
             }
         };
-        if (!kahan) {
+        if constexpr (LEAN) {
+            plain(std::false_type{});
+        } else if (!kahan) {
             if (dropping) plain(std::true_type{});
             else plain(std::false_type{});
         } else {
@@ -550,6 +557,63 @@ __global__ __launch_bounds__(256) void k_edge_grp(
             if (k + U < e1) consume(k + U, vb, sb);
 #pragma unroll
             for (int t = 0; t < CL; ++t) cb[t] = cb2[t];
+        }
+    } else if constexpr (RC == 2) {
+        // the ids as RC = 1, and the gathers one chunk ahead: chunk t+1's rows
+        // are in flight while chunk t is scored and accumulated.  The wave
+        // walks the chunk count of its longest row (wave-uniform, so the
+        // prefetch branch is scalar); consume() is spelled out in both arms of
+        // that branch, so the wait for chunk t's rows counts chunk t+1's loads
+        // (a shared join would wait for all of them).  Groups whose row is
+        // shorter gather clamped ids (their last edge) and skip consume (an
+        // empty row keeps m = -inf, l = 0, acc = 0).
+        constexpr int NQ = G / 4, R = 8 / NQ > 0 ? 8 / NQ : 1, NB = NQ * R;
+        const int qd = (c >> 2) & (NQ - 1), pq = c & 3;
+        int nchw = (e1 - e0 + U - 1) / U;
+#pragma unroll
+        for (int off = G; off < kWave; off <<= 1) nchw = max(nchw, __shfl_xor(nchw, off));
+        nchw = __builtin_amdgcn_readfirstlane(nchw);
+        f32x4 va[U][V], vb[U][V];
+        float sa[U], sb[U];
+        for (int i0 = 0; i0 < nchw; i0 += NB) {
+            const int b0 = e0 + i0 * U;
+            int cr[R];
+#pragma unroll
+            for (int q = 0; q < R; ++q)
+                cr[q] = col[min(b0 + U * (NQ * q + qd) + pq, max(e1 - 1, 0))];
+            auto ids = [&](int t, int (&cc)[CL]) {
+                if constexpr (NQ == 1) cc[0] = cr[t];
+                else cc[0] = __shfl(cr[t / NQ], gbase + 4 * (t % NQ) + pq);
+            };
+            const int nb = min(NB, nchw - i0);  // wave-uniform chunks in this batch
+            {
+                int cc[CL];
+                ids(0, cc);
+                fetch(cc, va, sa);
+            }
+#pragma unroll
+            for (int t = 0; t < NB; t += 2) {  // chunk t in set A, chunk t+1 in set B
+                if (t >= nb) break;
+                const int ka = b0 + U * t, kb = ka + U;
+                if (t + 1 < nb) {
+                    int cc[CL];
+                    ids(t + 1, cc);
+                    fetch(cc, vb, sb);
+                    if (ka < e1) consume(ka, va, sa);
+                } else {
+                    if (ka < e1) consume(ka, va, sa);
+                    break;
+                }
+                if (t + 2 < nb) {
+                    int cc[CL];
+                    ids(t + 2, cc);
+                    fetch(cc, va, sa);
+                    if (kb < e1) consume(kb, vb, sb);
+                } else {
+                    if (kb < e1) consume(kb, vb, sb);
+                    break;
+                }
+            }
         }
     } else if constexpr (RC > 0) {
         // ids of up to 8 chunks per round trip (see RC above)
@@ -809,31 +873,40 @@ __global__ __launch_bounds__(256) void k_edge_merge_wg(
 // never.  (Gathers one chunk ahead on top of it, round 6: 26.1 vs 25.1 us at
 // PPI, 100 VGPRs; profiles/r06/edge_ab_rc_pipelined_ppi.json; removed.)
 // ---------------------------------------------------------------------------
-static bool rowcol_for(int edges_per_row_hint) {
+// 0: one chunk ahead; 1: row-batched ids; 2: + the gathers one chunk ahead,
+// lean (the default where GAT_HINT_SHORT holds and the launch is an eval
+// forward; else 1).  PPI edge kernel, same box, graph-timed: 26.45 / 25.25 /
+// 25.00 us and 25.59 / 25.15 us for 1 / 2 in a second run; the lean row-batched
+// form without the gathers ahead (64 VGPRs, 8 waves per SIMD) 25.96 / 25.91 us
+// (profiles/r06/edge_ab_lean_ppi.json).
+static int rowcol_for(int edges_per_row_hint) {
     const char* v = knob("GAT_EDGE_ROWCOL");
-    return (v == nullptr || std::atoi(v) != 0) && edges_per_row_hint >= 16;
+    const int m = v == nullptr ? 2 : std::max(0, std::min(2, std::atoi(v)));
+    return edges_per_row_hint >= 16 ? m : 0;
 }
 
 constexpr bool fast_group(int g, int v) { return (g == 4 || g == 8 || g == 16) && (v == 1 || g <= 8); }
 
 // one launch of the fused kernel with the head's lane count as a constant
 // (hl = 1 or 2) or read at run time (HL = 0)
-template <int G, int U, int V, bool PIPE, bool KINK, int S, int RC, class... A>
+template <int G, int U, int V, bool PIPE, bool KINK, int S, int RC, bool LEAN = false,
+          class... A>
 static void launch_hl(int hl, dim3 grid, dim3 block, hipStream_t st, A... a) {
     if constexpr (fast_group(G, V)) {
         if (hl == 1) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1, 0, RC>), grid, block, 0,
-                               st, a...);
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 1, 0, RC, LEAN>), grid,
+                               block, 0, st, a...);
             return;
         }
         if (hl == 2) {
-            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 2, 0, RC>), grid, block, 0,
-                               st, a...);
+            hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 2, 0, RC, LEAN>), grid,
+                               block, 0, st, a...);
             return;
         }
     }
-    hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 0, 0, RC>), grid, block, 0, st,
-                       a...);
+    if constexpr (!LEAN)
+        hipLaunchKernelGGL((k_edge_grp<G, U, V, true, PIPE, KINK, S, 0, 0, RC>), grid, block, 0,
+                           st, a...);
 }
 
 // the fused kernel on a fast lane group; u, rc, pipe and split as the
@@ -850,6 +923,9 @@ static void launch_fast(int u, int rc, int pipe, int split, int hl, dim3 grid, d
                 if (split == 4) return launch_hl<G, 4, V, false, false, 4, 0>(hl, dim3(grid.x * 4), block, st, a...);
             }
             if constexpr (G != 4) {  // (row-batched ids: G = 8, 16)
+                if constexpr (!KINK && V == 1) {
+                    if (rc == 2) return launch_hl<G, 4, V, false, false, 1, 2, true>(hl, grid, block, st, a...);
+                }
                 if (rc) return launch_hl<G, 4, V, false, KINK, 1, 1>(hl, grid, block, st, a...);
             }
             return launch_hl<G, 4, V, false, KINK, 1, 0>(hl, grid, block, st, a...);
@@ -952,7 +1028,8 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
     // narrow row-major rows then take two float4s per lane (16 rows per wave at
     // HF = 32: CIFAR batch 11.6 -> 8.6 us; a uniform graph gains nothing)
     const bool local_hint = edges_per_row_hint > 0 && (edges_per_row_hint & GAT_HINT_LOCAL);
-    edges_per_row_hint &= ~GAT_HINT_LOCAL;
+    const bool short_hint = edges_per_row_hint > 0 && (edges_per_row_hint & GAT_HINT_SHORT);
+    edges_per_row_hint &= ~(GAT_HINT_LOCAL | GAT_HINT_SHORT);
     int vv = edges_per_row_hint >= 128 ? 2 : 1;
     if (local_hint && !sliced && round_up4(hf) <= 32) vv = 2;
     if (const char* ev = knob("GAT_EDGE_V")) vv = std::atoi(ev) >= 2 ? 2 : 1;
@@ -1021,7 +1098,11 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         }
         if (kink || pipe) split = 1;
         if ((long long)blocks * split >= (1LL << 31)) split = 1;
-        bool rc = rowcol_for(edges_per_row_hint);
+        int rc = rowcol_for(edges_per_row_hint);
+        // the lean forms: eval, whole rows or hub-free schedules, rows < 1024
+        const bool lean_ok = short_hint && !kink && lse == nullptr && y_heads == nullptr &&
+                             drop.thresh == 0u && vv == 1;
+        if (rc >= 2 && !lean_ok) rc = 1;
         // the instances that exist (see above): everything off the fast lane
         // groups, other head widths and the gathered-score form run U = 8, one
         // group per row, no row-batched ids, no pipelining
@@ -1032,7 +1113,7 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
             pipe = 0;
         }
         if (vv == 2 && u == 8) u = 4;  // V = 2 below U = 16: local narrow rows
-        if (u != 4 || g == 4) rc = false;
+        if (u != 4 || g == 4) rc = 0;
         const XProjArgs xpa = xp != nullptr ? *xp : XProjArgs{nullptr, nullptr, nullptr, nullptr,
                                                               nullptr, 0};
 #define GAT_GRP_KARGS                                                                         \

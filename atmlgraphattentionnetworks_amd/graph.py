@@ -53,9 +53,16 @@ class CSRGraph(NamedTuple):
 
     def kernel_hint(self) -> int:
         """The edge kernels' scheduling hint: E'/N, with GAT_HINT_LOCAL OR'd in
-        for a local graph (include/gat_amd.h)."""
+        for a local graph and GAT_HINT_SHORT when every row has fewer than
+        1024 in-edges (include/gat_amd.h)."""
         h = self.num_edges // max(self.num_nodes, 1)
-        return h | _lib.GAT_HINT_LOCAL if self.local and h > 0 else h
+        if h <= 0:
+            return h
+        if self.local:
+            h |= _lib.GAT_HINT_LOCAL
+        if 0 < self.max_degree < 1024:
+            h |= _lib.GAT_HINT_SHORT
+        return h
 
 
 def _check_edge_index(edge_index: torch.Tensor, device: torch.device) -> torch.Tensor:

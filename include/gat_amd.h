@@ -119,8 +119,9 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
  *   lse          optional [rows, heads] = max + log(sum exp) per (row, head)
  *                (natural log; for the backward pass); may be NULL
  *   edges_per_row_hint  average in-degree (E'/rows) or 0 if unknown: picks the
- *                edge-chunk length, never affects results; GAT_HINT_LOCAL may be
- *                OR'd in (every entry point taking a hint accepts it)
+ *                edge-chunk length, never affects results; GAT_HINT_LOCAL and
+ *                GAT_HINT_SHORT may be OR'd in (every entry point taking a hint
+ *                accepts them)
  * GAT_EUNSUPPORTED if s_src is NULL and the shape needs it (f % 4 != 0, or
  * f/4 not a power of two, or negative_slope outside [0, 1]).
  */
@@ -128,6 +129,11 @@ int gat_project(const float* x, int n, int fin, const float* w, const float* b,
  * (block-diagonal batches of small graphs, kNN graphs), so rows processed
  * together share source rows.  Never affects results. */
 #define GAT_HINT_LOCAL (1 << 30)
+/* Scheduling hint bit (ABI 11): every row or segment the call walks has fewer
+ * than 1024 in-edges, so the edge kernels may drop the Kahan-compensated sums
+ * they keep for longer rows (which shorter rows never use).  Never affects
+ * results when it holds. */
+#define GAT_HINT_SHORT (1 << 29)
 
 int gat_edge_aggregate(const int* rowptr, const int* col, const int* row_order, int row_begin,
                        int row_end, const float* wh, int ld_wh, const float* s_src, int ld_s,
