@@ -222,9 +222,16 @@ class SchedCSR(NamedTuple):
 
 
 SCHED_MAX_EPR = 64  # scheduled copy below this many in-edges per row (E'/N)
+STAGGER_MIN_EPR = 16  # staggered sweeps from this many in-edges per row
 
 
-def build_sched_csr(csr: "CSRGraph") -> SchedCSR:
+def build_sched_csr(csr: "CSRGraph", stagger: bool = False) -> SchedCSR:
+    """The scheduled copy.  ``stagger``: schedule position p's in-edges (sources
+    ascending) are rotated to start at the first source >= p and wrap around,
+    so the rows the kernel runs at one time sweep the node table from offsets
+    that advance with their position in the schedule (roughly their start
+    time) instead of all from node 0.  The same edges in another order:
+    results equal up to fp32 summation order."""
     rp = csr.rowptr.to(torch.int64)
     order = csr.order.to(torch.int64)
     n = csr.num_nodes
@@ -232,11 +239,19 @@ def build_sched_csr(csr: "CSRGraph") -> SchedCSR:
     sptr = torch.zeros(n + 1, dtype=torch.int64, device=rp.device)
     sptr[1:] = deg.cumsum(0)
     e = csr.num_edges  # output sizes given: no device -> host sync (graph-capture safe)
-    offs = torch.arange(e, device=rp.device) - torch.repeat_interleave(sptr[:-1], deg,
-                                                                         output_size=e)
+    b_rep = torch.repeat_interleave(sptr[:-1], deg, output_size=e)
+    offs = torch.arange(e, device=rp.device) - b_rep
     idx = torch.repeat_interleave(rp[order], deg, output_size=e) + offs
+    col = csr.col[idx]
+    if stagger and n > 0:
+        # (sources are node ids in [0, n): position p's sweep starts at node p)
+        pos = torch.repeat_interleave(torch.arange(n, device=rp.device), deg, output_size=e)
+        below = (col.to(torch.int64) < pos).to(torch.int64)
+        rot = torch.zeros(n, dtype=torch.int64, device=rp.device).index_add_(0, pos, below)
+        d_rep = torch.repeat_interleave(deg.clamp(min=1), deg, output_size=e)
+        col = col[b_rep + (offs + rot[pos]) % d_rep]
     return SchedCSR(sptr[:-1].to(torch.int32).contiguous(), sptr[1:].to(torch.int32).contiguous(),
-                    csr.col[idx].contiguous())
+                    col.contiguous())
 
 
 _sched_cache = {}
@@ -247,7 +262,7 @@ def sched_csr(csr: "CSRGraph") -> Optional[SchedCSR]:
     kept while ``csr.rowptr`` lives), or None: long rows (E'/N >=
     SCHED_MAX_EPR: the prologue is a small share, and the copy would double a
     large col array), split hub rows (they have their own schedule), no row
-    order, or GAT_EDGE_SCHED=0 (A/B knob).  Costs E' * 4 + N * 8 bytes."""
+    order, or GAT_EDGE_SCHED=0 (knob).  Costs E' * 4 + N * 8 bytes."""
     if (tuning.get("GAT_EDGE_SCHED") == "0" or csr.order is None or csr.hubs is not None
             or csr.num_nodes == 0 or csr.num_edges // csr.num_nodes >= SCHED_MAX_EPR):
         return None
@@ -255,7 +270,11 @@ def sched_csr(csr: "CSRGraph") -> Optional[SchedCSR]:
     hit = _sched_cache.get(key)
     if hit is not None and hit[0]() is csr.rowptr:
         return hit[1]
-    sc = build_sched_csr(csr)
+    # staggered sweeps where rows average >= 16 in-edges (PPI: layer step
+    # 33.92 -> 33.18 us, same box; arxiv's 8 per row 81.18 -> 81.65 us:
+    # profiles/r06/step_ab_stagger.json); GAT_EDGE_SCHED=plain: never
+    sc = build_sched_csr(csr, stagger=tuning.get("GAT_EDGE_SCHED") != "plain"
+                         and csr.num_edges // csr.num_nodes >= STAGGER_MIN_EPR)
     _sched_cache[key] = (weakref.ref(csr.rowptr), sc)
     weakref.finalize(csr.rowptr, _sched_cache.pop, key, None)
     return sc

@@ -47,8 +47,10 @@ VARIANTS = {
     # Fin <= 4: projection and edge kernel as two launches instead of the fused
     # small-Fin kernel (the default through gat_layer_forward)
     "no_xproj": {"GAT_EDGE_XPROJ": "0"},
-    # the CSR-order launch (short rows take the scheduled copy by default)
+    # the CSR-order launch (short rows take the scheduled copy by default), and
+    # the scheduled copy without the staggered sweeps
     "nosched": {"GAT_EDGE_SCHED": "0"},
+    "sched_plain": {"GAT_EDGE_SCHED": "plain"},
     # sliced node table (gat_*_sliced); shapes it does not take run row-major
     "sliced2": {"GAT_WH_SLICES": "2"},
 }

@@ -24,7 +24,10 @@ SETTINGS = dict(deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @st.composite
 def graphs(draw, max_nodes=40, max_edges=300):
     n = draw(st.integers(1, max_nodes))
-    e = draw(st.integers(0, max_edges))
+    # at most ~400 in-edges per row on average: a row of thousands of edges
+    # sums that many terms, where the fp32 reference itself drifts past the
+    # 1e-5 bar (such rows are checked against float64 in tests/test_gpu_hubs.py)
+    e = draw(st.integers(0, min(max_edges, 400 * n)))
     seed = draw(st.integers(0, 2**31 - 1))
     rng = np.random.default_rng(seed)
     ei = torch.from_numpy(rng.integers(0, n, size=(2, e)).astype(np.int64))

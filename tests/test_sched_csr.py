@@ -29,3 +29,18 @@ def test_sched_csr_positions_hold_their_rows():
         r = order[p]
         assert (scol[b[p]:e[p]] == col[rp[r]:rp[r + 1]]).all()
     assert sc.b.dtype == sc.e.dtype == sc.col.dtype == torch.int32
+
+
+def test_staggered_sched_csr_rotates_each_row():
+    """stagger=True: position p holds the same in-edges as its row, ascending
+    from the first source >= p and wrapping around (a rotation of the sorted
+    list), so a rows' sweep starts at node p."""
+    csr = _csr(700, 14000, 5)
+    plain, stag = build_sched_csr(csr), build_sched_csr(csr, stagger=True)
+    assert torch.equal(plain.b, stag.b) and torch.equal(plain.e, stag.e)
+    b, e = plain.b.numpy(), plain.e.numpy()
+    pc, sc = plain.col.numpy(), stag.col.numpy()
+    for p in range(csr.num_nodes):
+        row, got = pc[b[p]:e[p]], sc[b[p]:e[p]]
+        r = int((row < p).sum())
+        assert (got == np.concatenate([row[r:], row[:r]])).all(), p

@@ -221,6 +221,8 @@ def main():
 
     def plan_for(env):
         env = dict(env)
+        from atmlgraphattentionnetworks_amd import graph as _graph
+        _graph._sched_cache.clear()  # the scheduled copy is built under each variant's knobs
         if int(env.pop("hublast", "0")):
             apply(env)
             plan = ForwardPlan(x, csr, w.heads, w.out_channels, w.concat, 0.2)
