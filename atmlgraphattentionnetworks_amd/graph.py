@@ -223,6 +223,7 @@ class SchedCSR(NamedTuple):
 
 SCHED_MAX_EPR = 64  # scheduled copy below this many in-edges per row (E'/N)
 STAGGER_MIN_EPR = 16  # staggered sweeps from this many in-edges per row
+ROTATE_STRIDE = 2  # long rows: schedule position p's sweep starts at node 2p mod N
 
 
 def build_sched_csr(csr: "CSRGraph", stagger: bool = False) -> SchedCSR:
@@ -254,7 +255,52 @@ def build_sched_csr(csr: "CSRGraph", stagger: bool = False) -> SchedCSR:
                     col.contiguous())
 
 
+def rotate_rows(csr: "CSRGraph", stride: int) -> torch.Tensor:
+    """``csr.col`` with each row rotated to start at its first source >=
+    (schedule position * stride) mod N and wrap around: the rows the kernel
+    runs at one time then sweep the node table from offsets that advance with
+    their start time.  CSR row order kept (so ``rowptr`` and the hub schedule
+    still index it); the same edges in another order within each row."""
+    rp = csr.rowptr.to(torch.int64)
+    n, e = csr.num_nodes, csr.num_edges
+    dev = rp.device
+    pos = torch.empty(n, dtype=torch.int64, device=dev)
+    pos[csr.order.to(torch.int64)] = torch.arange(n, device=dev)
+    deg = rp[1:] - rp[:-1]
+    row = torch.repeat_interleave(torch.arange(n, device=dev), deg, output_size=e)
+    start = (pos * stride) % n
+    below = (csr.col.to(torch.int64) < start[row]).to(torch.int64)
+    rot = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, row, below)
+    base = rp[:-1][row]
+    offs = torch.arange(e, device=dev) - base
+    return csr.col[base + (offs + rot[row]) % deg.clamp(min=1)[row]].contiguous()
+
+
 _sched_cache = {}
+_rot_cache = {}
+
+
+def rotated_col(csr: "CSRGraph") -> torch.Tensor:
+    """The col array the eval forward walks for LONG rows (E'/N >=
+    SCHED_MAX_EPR, where no scheduled copy is built): ``rotate_rows`` with
+    stride ROTATE_STRIDE, built on first use and kept while ``csr.rowptr``
+    lives (E' * 4 bytes).  Reddit layer step 2.011 -> 1.959 ms, power-law
+    Reddit 2.261 -> 2.238 ms; strides 1 / 4 / 6 / 8 / 16: 1.982 / 1.961 /
+    1.981 / 2.074 / 3.021 ms (profiles/r06/step_ab_rotate_long_rows.json).  Returns
+    ``csr.col`` itself for short rows, no row order, or GAT_EDGE_SCHED=plain."""
+    if (tuning.get("GAT_EDGE_SCHED") == "plain" or csr.order is None or csr.num_nodes == 0
+            or csr.num_edges // csr.num_nodes < SCHED_MAX_EPR):
+        return csr.col
+    key = id(csr.rowptr)
+    hit = _rot_cache.get(key)
+    if hit is not None and hit[0]() is csr.rowptr:
+        return hit[1]
+    col = rotate_rows(csr, ROTATE_STRIDE)
+    _rot_cache[key] = (weakref.ref(csr.rowptr), col)
+    weakref.finalize(csr.rowptr, _rot_cache.pop, key, None)
+    return col
+
+
 
 
 def sched_csr(csr: "CSRGraph") -> Optional[SchedCSR]:

@@ -28,7 +28,7 @@ from typing import NamedTuple, Optional, Tuple
 import torch
 
 from . import _lib, tuning
-from .graph import CSRGraph, get_csr, sched_csr
+from .graph import CSRGraph, get_csr, rotated_col, sched_csr
 
 __all__ = ["GraphAttentionLayer", "GraphAttentionLayerActivationTest", "score_activation_code",
            "PackedParams", "pack_params", "gat_forward", "ForwardPlan", "wh_slices", "NodeTable",
@@ -280,7 +280,7 @@ def _edge_hubs(lib, csr: CSRGraph, wh_ptr: int, ld_wh: int, n_table: int, slices
                negative_slope: float, bias: torch.Tensor, out: torch.Tensor, stream: int) -> None:
     """Edge kernel with the hub rows split (graph.HubPlan): one launch over the
     hub segments (state stored) and the whole rows (output written), then
-    gat_edge_merge for the hubs."""
+    gat_edge_merge for the hubs.  Rows walk graph.rotated_col (long rows)."""
     hubs = csr.hubs
     hf4 = (heads * f + 3) // 4 * 4
     nv = hubs.n_vrows
@@ -291,7 +291,7 @@ def _edge_hubs(lib, csr: CSRGraph, wh_ptr: int, ld_wh: int, n_table: int, slices
     hint = csr.kernel_hint() if hasattr(csr, "kernel_hint") else \
         csr.num_edges // max(csr.num_nodes, 1)
     rc = lib.gat_edge_aggregate_seg(
-        hubs.sched_b.data_ptr(), hubs.sched_e.data_ptr(), 1, csr.col.data_ptr(),
+        hubs.sched_b.data_ptr(), hubs.sched_e.data_ptr(), 1, rotated_col(csr).data_ptr(),
         hubs.sched_row.data_ptr(), 0, n_pos, wh_ptr, ld_wh, n_table, slices,
         pp.a_src.data_ptr(), pp.c_src.data_ptr(), p_sd, heads, f, int(concat),
         float(negative_slope), p_acc, p_ml, 0, nv, bias.data_ptr(), out.data_ptr(), hint, stream)
@@ -455,7 +455,9 @@ class ForwardPlan:
 
     def edge(self, lib, csr: CSRGraph, pp: PackedParams, bias: torch.Tensor,
              out: torch.Tensor) -> torch.Tensor:
-        """The edge kernel(s) over the table project() wrote (GAT.py:53-67, +bias)."""
+        """The edge kernel(s) over the table project() wrote (GAT.py:53-67, +bias).
+        Short rows walk the scheduled copy (graph.sched_csr), long rows the
+        rotated col array (graph.rotated_col): the same edges per row."""
         n, heads, f = self.n, self.heads, self.f
         stream = torch._C._cuda_getCurrentRawStream(self.dev)
         if self.split:
@@ -477,14 +479,14 @@ class ForwardPlan:
             return out
         if self.slices > 1:
             rc = lib.gat_edge_aggregate_sliced(
-                csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, self.p_wh, n,
+                csr.rowptr.data_ptr(), rotated_col(csr).data_ptr(), p_order, 0, n, self.p_wh, n,
                 self.slices, pp.a_src.data_ptr(), pp.c_src.data_ptr(), self.p_sd, heads, f,
                 self.slope, bias.data_ptr(), out.data_ptr(), self.khint, stream)
             if rc:
                 _lib.check(rc, "gat_edge_aggregate_sliced")
             return out
         rc = lib.gat_edge_aggregate(
-            csr.rowptr.data_ptr(), csr.col.data_ptr(), p_order, 0, n, self.p_wh, self.hfp,
+            csr.rowptr.data_ptr(), rotated_col(csr).data_ptr(), p_order, 0, n, self.p_wh, self.hfp,
             self.p_ss if self.need_ss else 0, heads, pp.a_src.data_ptr(), pp.c_src.data_ptr(),
             self.p_sd, heads, f,
             int(self.concat), self.slope, bias.data_ptr(), out.data_ptr(), 0, self.khint, stream)

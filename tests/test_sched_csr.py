@@ -4,7 +4,8 @@ positions tile the copy contiguously.  Host logic only (CPU tensors)."""
 import numpy as np
 import torch
 
-from atmlgraphattentionnetworks_amd.graph import CSRGraph, build_sched_csr
+from atmlgraphattentionnetworks_amd import graph
+from atmlgraphattentionnetworks_amd.graph import CSRGraph, build_sched_csr, rotate_rows, rotated_col
 
 
 def _csr(n, e, seed):
@@ -44,3 +45,38 @@ def test_staggered_sched_csr_rotates_each_row():
         row, got = pc[b[p]:e[p]], sc[b[p]:e[p]]
         r = int((row < p).sum())
         assert (got == np.concatenate([row[r:], row[:r]])).all(), p
+
+
+def test_rotated_rows_keep_csr_order():
+    """rotate_rows: row r (schedule position p) keeps its CSR slot and holds
+    its in-edges ascending from the first source >= stride * p mod N, wrapping
+    around."""
+    csr = _csr(600, 9000, 7)
+    rp, col, order = csr.rowptr.numpy(), csr.col.numpy(), csr.order.numpy()
+    for stride in (1, 2, 5):
+        rot = rotate_rows(csr, stride).numpy()
+        assert rot.dtype == np.int32 and rot.shape == col.shape
+        for p, r in enumerate(order):
+            row, got = col[rp[r]:rp[r + 1]], rot[rp[r]:rp[r + 1]]
+            k = int((row < (stride * p) % csr.num_nodes).sum())
+            assert (got == np.concatenate([row[k:], row[:k]])).all(), (stride, p)
+
+
+def test_rotated_col_only_for_long_rows(monkeypatch):
+    """Short rows (E'/N < SCHED_MAX_EPR) walk csr.col (their scheduled copy is
+    staggered instead); long rows a cached rotated copy; GAT_EDGE_SCHED=plain
+    turns it off."""
+    short = _csr(300, 3000, 1)
+    assert rotated_col(short) is short.col
+    long_ = _csr(100, 100 * graph.SCHED_MAX_EPR, 2)
+    a = rotated_col(long_)
+    assert a is not long_.col and rotated_col(long_) is a
+    assert torch.equal(a, rotate_rows(long_, graph.ROTATE_STRIDE))
+    monkeypatch.setenv("GAT_EDGE_SCHED", "plain")
+    from atmlgraphattentionnetworks_amd import tuning
+    tuning.reload()
+    try:
+        assert rotated_col(long_) is long_.col
+    finally:
+        monkeypatch.delenv("GAT_EDGE_SCHED")
+        tuning.reload()
