@@ -400,13 +400,46 @@ def build_csc(csr: CSRGraph) -> CSCGraph:
 _csc_cache = {}
 
 
+CSC_ROTATE_STRIDE = 8  # long rows: source j's out-edges start at target 8j mod N
+
+
+def rotate_csc(csc: CSCGraph, n: int, e: int, stride: int) -> CSCGraph:
+    """Staggered sweeps for the backward source pass (``gat_bwd_sources`` walks
+    source rows in node order): source j's CSC slots rotated to start at its
+    first target >= stride * j mod N and wrap around, ``dst`` and ``eid``
+    together, ``csr_to_csc`` re-inverted.  The same out-edges per source in
+    another order (gradients equal up to fp32 summation order).  Reddit
+    training step (dropout 0.6) 8.65 -> 8.46 ms at stride 8; strides 1 / 2 /
+    4 / 16 / 64: 8.59 / 8.60 / 8.49 / 8.61 / 9.04 ms
+    (profiles/r06/train_ab_csc_rotate_reddit.json)."""
+    ptr = csc.ptr.to(torch.int64)
+    dev = ptr.device
+    deg = ptr[1:] - ptr[:-1]
+    row = torch.repeat_interleave(torch.arange(n, device=dev), deg, output_size=e)
+    start = (torch.arange(n, device=dev) * stride) % max(n, 1)
+    below = (csc.dst.to(torch.int64) < start[row]).to(torch.int64)
+    rot = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, row, below)
+    base = ptr[:-1][row]
+    src = base + (torch.arange(e, device=dev) - base + rot[row]) % deg.clamp(min=1)[row]
+    del row, start, below, base
+    eid = csc.eid[src].contiguous()
+    c2c = torch.empty_like(csc.csr_to_csc)
+    c2c[eid.to(torch.int64)] = torch.arange(e, device=dev, dtype=torch.int32)
+    return CSCGraph(csc.ptr, csc.dst[src].contiguous(), eid, c2c)
+
+
 def get_csc(csr: CSRGraph) -> CSCGraph:
-    """The CSC of ``csr``, built on first use and kept while ``csr.rowptr`` lives."""
+    """The CSC of ``csr``, built on first use and kept while ``csr.rowptr`` lives;
+    long rows (E'/N >= SCHED_MAX_EPR) get ``rotate_csc`` (GAT_EDGE_SCHED=plain:
+    never)."""
     key = id(csr.rowptr)
     hit = _csc_cache.get(key)
     if hit is not None and hit[0]() is csr.rowptr:
         return hit[1]
     csc = build_csc(csr)
+    if (tuning.get("GAT_EDGE_SCHED") != "plain" and csr.num_nodes > 0
+            and csr.num_edges // csr.num_nodes >= SCHED_MAX_EPR):
+        csc = rotate_csc(csc, csr.num_nodes, csr.num_edges, CSC_ROTATE_STRIDE)
     _csc_cache[key] = (weakref.ref(csr.rowptr), csc)
     weakref.finalize(csr.rowptr, _csc_cache.pop, key, None)
     return csc

@@ -378,27 +378,35 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
     return res
 
 
-def _graph_step_ms(step, warmup: int, steps: int):
-    """ms per ``step`` replayed from a captured graph (None if capture fails)."""
+def _graph_step_ms(step, warmup: int, steps: int, per_replay: int = 2):
+    """ms per ``step`` replayed from a captured graph (None if capture fails).
+    ``per_replay`` consecutive steps are captured into one graph: with the
+    layer's two ping-pong workspaces a one-step graph would replay the same
+    workspace every time (the projection writing the table the previous
+    replay's edge kernel read), and the sharded graphs
+    (distributed.capture_steps) hold two steps per replay as well."""
     try:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            step()
+            for _ in range(per_replay):
+                step()
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            step()
+            for _ in range(per_replay):
+                step()
     except Exception:  # noqa: BLE001  (the eager number stands alone)
         return None
-    for _ in range(warmup):
+    reps = max(1, steps // per_replay)
+    for _ in range(max(1, warmup // per_replay)):
         g.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(reps):
         g.replay()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) * 1e3 / steps
+    return (time.perf_counter() - t0) * 1e3 / (reps * per_replay)
 
 
 def fused_small_fin(fin: int, plan) -> bool:

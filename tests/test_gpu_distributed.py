@@ -347,6 +347,8 @@ def test_bench_dist_one_rank_rccl(tmp_path):
     assert d["value"] >= g["value"] * (1 - 1e-9)
     og = d["one_gpu_same_workload"]
     assert og["launch"] == "eager" and og["graph"]["ok"]
+    # both graph sides hold the same number of steps per replay
+    assert g["launch"].startswith(og["graph"]["launch"]), (og["graph"]["launch"], g["launch"])
     if "eager" in head:  # the graph won: its speed-up is over the graphed one-GPU step
         assert d["value"] == g["value"] and d["config"]["launch"].startswith("hipGraph")
         assert d["speedup_launch_mode"] == "hipGraph vs hipGraph"
