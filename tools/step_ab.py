@@ -5,7 +5,7 @@ environment variants, in ONE process.  A variant is ``name:K=V,K=V`` (knobs,
 or any variable the layer reads when it builds its cached plan); each round
 builds a fresh layer per variant from the same parameters.
 
-    python tools/step_ab.py --workload ppi --rounds 5 --variants "base:;nb3:GAT_EXP_NBUF=3"
+    python tools/step_ab.py --workload ppi --rounds 5 --variants "base:;plain:GAT_EDGE_SCHED=plain"
 """
 import argparse
 import json
