@@ -4,7 +4,9 @@ linear in the gathered rows ``x_j`` (``GAT.py:62``, ``aggr='add'``), and the
 edge order does not matter.  ``hypothesis`` draws the graphs and shapes.
 
 CPU: on the oracle's restatement of ``propagate`` (``oracle/gat_oracle.py``).
-GPU (``-m gpu``): on the HIP kernels through the C-ABI.  ``gat_edge_aggregate``
+GPU (``-m gpu``): on the HIP kernels through the C-ABI, and for the training
+backward: linearity in the upstream gradient and edge-order invariance of the
+gradients.  ``gat_edge_aggregate``
 with an ``s_src`` table and no ``a_src`` runs the gathered-score kernels, so
 the scores can be drawn independently of the rows they weight: rows of ones
 give sum(alpha) per (target, head) exactly.
@@ -174,3 +176,71 @@ def test_hip_layer_invariant_to_edge_order(g, hf, concat):
     assert torch.equal(a, b)
     ref = gat_layer_forward_from_state(state, x, ei, heads, concat)
     torch.testing.assert_close(a, ref, atol=1e-5, rtol=1e-5)
+
+
+def _layer_grads(layer, x, ei, gout):
+    layer.zero_grad()
+    xd = x.detach().clone().requires_grad_(True)
+    out = layer(xd, ei)
+    (out * gout).sum().backward()
+    return [xd.grad.clone()] + [p.grad.clone() for p in layer.parameters()]
+
+
+@pytest.mark.gpu
+@settings(max_examples=15, **SETTINGS)
+@given(g=graphs(max_nodes=300, max_edges=9000), hf=st.sampled_from([(8, 8), (4, 16), (2, 5)]),
+       concat=st.booleans(), c=st.floats(-2.0, 2.0))
+def test_hip_backward_linear_in_upstream_gradient(g, hf, concat, c):
+    """The HIP backward (recompute form, or the stored form for F = 5) is linear
+    in dL/dout: grads(g1 + c g2) = grads(g1) + c grads(g2), to fp32 rounding
+    (run_inductive.py:84-85's loss.backward() through GAT.py:37-67)."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    n, ei, rng = g
+    heads, f = hf
+    d = _dev()
+    fin = 10
+    state = init_reference_params(fin, f, heads, concat, seed=int(rng.integers(1 << 30)))
+    layer = GraphAttentionLayer(fin, f, num_heads=heads, concat=concat, dropout=0.0)
+    layer.load_state_dict(state)
+    layer = layer.to(d).train()
+    x = torch.from_numpy(rng.standard_normal((n, fin)).astype(np.float32)).to(d)
+    eid = ei.to(d)
+    width = heads * f if concat else f
+    g1 = torch.from_numpy(rng.standard_normal((n, width)).astype(np.float32)).to(d)
+    g2 = torch.from_numpy(rng.standard_normal((n, width)).astype(np.float32)).to(d)
+    a = _layer_grads(layer, x, eid, g1)
+    b = _layer_grads(layer, x, eid, g2)
+    ab = _layer_grads(layer, x, eid, g1 + c * g2)
+    # sums whose terms cancel (the attention-vector gradients: sum over a
+    # softmax of dz, exactly 0 for a row with one in-edge) carry fp32 noise
+    # at the scale of their terms, not of the result: a floor from the
+    # largest gradient of the call
+    floor = 1e-6 * max(float(t.abs().max()) for t in a + b) * (1.0 + abs(c))
+    for u, v, w in zip(a, b, ab):
+        ref = u + c * v
+        scale = float(u.abs().max() + abs(c) * v.abs().max())
+        torch.testing.assert_close(w, ref, atol=2e-5 * scale + floor, rtol=0)
+
+
+@pytest.mark.gpu
+@settings(max_examples=10, **SETTINGS)
+@given(g=graphs(max_nodes=300, max_edges=9000), concat=st.booleans())
+def test_hip_backward_invariant_to_edge_order(g, concat):
+    """Gradients of the layer on a permuted edge_index: bit for bit the same (the
+    CSR and CSC group edges with stable sorts; dropout 0)."""
+    from atmlgraphattentionnetworks_amd import GraphAttentionLayer
+    n, ei, rng = g
+    heads, f, fin = 8, 8, 10
+    d = _dev()
+    state = init_reference_params(fin, f, heads, concat, seed=int(rng.integers(1 << 30)))
+    layer = GraphAttentionLayer(fin, f, num_heads=heads, concat=concat, dropout=0.0)
+    layer.load_state_dict(state)
+    layer = layer.to(d).train()
+    x = torch.from_numpy(rng.standard_normal((n, fin)).astype(np.float32)).to(d)
+    width = heads * f if concat else f
+    gout = torch.from_numpy(rng.standard_normal((n, width)).astype(np.float32)).to(d)
+    perm = torch.from_numpy(rng.permutation(ei.size(1)))
+    a = _layer_grads(layer, x, ei.to(d), gout)
+    b = _layer_grads(layer, x, ei[:, perm].contiguous().to(d), gout)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
