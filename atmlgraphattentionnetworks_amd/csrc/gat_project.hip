@@ -498,8 +498,26 @@ __global__ __launch_bounds__(256, MINB) void k_project_x3(
 #pragma unroll
             for (int q = 0; q < XL; ++q) {
                 const int e = (tid + NTH * q) * LW;
+                vec v = xn[q];
+                if constexpr (LW == 4) {
+                    // fin % 4 != 0 (8-B aligned rows): the load for position p was
+                    // clamped to fin - 4; its elements d = p - (fin - 4) on are
+                    // this position's, and elements past fin are zero
+                    const int p = k0 + e % BK, d = p - min(p, fin - 4);
+                    if (d == 1) v = f32x4{v.y, v.z, v.w, 0.f};
+                    else if (d == 2) v = f32x4{v.z, v.w, 0.f, 0.f};
+                    else if (d == 3) v = f32x4{v.w, 0.f, 0.f, 0.f};
+                    else if (d != 0) v = f32x4{0.f, 0.f, 0.f, 0.f};
+                    const int rem = fin - p;  // elements of this row from p on
+                    if (rem < 4) {
+                        if (rem <= 0) v.x = 0.f;
+                        if (rem <= 1) v.y = 0.f;
+                        if (rem <= 2) v.z = 0.f;
+                        v.w = 0.f;
+                    }
+                }
                 *reinterpret_cast<vec*>(xsm + (e / BK) * XS + e % BK) =
-                    k0 + e % BK < fin ? xn[q] : vec{};
+                    k0 + e % BK < fin ? v : vec{};
             }
         }
         if constexpr (PS) {
@@ -1249,7 +1267,13 @@ __global__ __launch_bounds__(256) void k_project_wk(
     }
 }
 
-// k_project_x3 on pre-split W (instantiated for 2 and 4 column tiles only)
+// k_project_x3 on pre-split W (instantiated for 2 and 4 column tiles only).  It
+// reads x as float4s for every even fin whose rows are 8-B aligned (Reddit's
+// 602: half the rows start 8 B into a 16-B unit; the loads need only dword
+// alignment), the last k chunk's clamped loads shifted into place in `stage`:
+// Reddit 191.7 -> 186.3 us, a P = 8 rank's share 30.9 -> 30.1 us, bitwise equal
+// outputs (profiles/r06/proj_ab_x3_float4_reddit.json); two chunks in flight
+// there: 216.6 us
 template <int NT, int LW, class... A>
 static void launch_x3_presplit(dim3 grid, dim3 block, hipStream_t st, A... a) {
     if constexpr (NT == 2 || NT == 4)
@@ -1391,7 +1415,7 @@ static int project_impl(const float* x, int n, int fin, const float* w, const fl
 #define GAT_X3_NT(NT)                                                                          \
     if (lw == 4) { GAT_X3(NT, 4, 1, 2, 1, 64); }                                               \
     else if (lw == 2 && presplit)                                                              \
-        launch_x3_presplit<NT, 2>(dim3((nr + 63) / 64, ny), bp, st, x, n, fin,                 \
+        launch_x3_presplit<NT, 4>(dim3((nr + 63) / 64, ny), bp, st, x, n, fin,                 \
                                   reinterpret_cast<const float*>(ws), b, a_src, c_src, a_dst,  \
                                   c_dst, heads, f, hf, wh, ld_wh, s_src, ld_s, s_dst, slice_w, \
                                   slice_stride, store_wt, crows, cjump);                       \
