@@ -937,8 +937,8 @@ static void launch_fast(int u, int rc, int pipe, int split, int hl, dim3 grid, d
             }
             return launch_hl<G, 8, V, false, KINK, 1, 0>(hl, grid, block, st, a...);
         }
-        if constexpr (V == 2) {
-            if (pipe) return launch_hl<G, 16, V, true, KINK, 1, 0>(hl, grid, block, st, a...);
+        if constexpr (V == 2 && !KINK) {
+            if (pipe) return launch_hl<G, 16, V, true, false, 1, 0>(hl, grid, block, st, a...);
         }
         launch_hl<G, 16, V, false, KINK, 1, 0>(hl, grid, block, st, a...);
     }
@@ -1075,6 +1075,10 @@ static int edge_aggregate_impl(const EdgeRows er, const int* col, const int* row
         const bool seg_pass = !er.by_pos && (er.load || er.store_lt > 0);
         int pipe = (u == 16 && vv == 2 && !seg_pass) ? 1 : 0;
         if (const char* ep = knob("GAT_EDGE_PIPE")) pipe = std::atoi(ep) != 0 && u == 16 && vv == 2;
+        // not the training forward (kink sums, dropout, lse / y): there the
+        // gathers one chunk ahead cost more than they hide (Reddit training
+        // step 8.45 -> 8.35 ms without, profiles/r06/train_ab_fwd_nopipe_reddit.json)
+        if (kink) pipe = 0;
         // two lane groups per row (the grid doubles inside launch_fast); the
         // kink-sum forward and the pipelined kernel keep one group.  Segment
         // passes (er.load / store_lt: hub segments, the sharded chunk passes) DO

@@ -128,7 +128,10 @@ def test_backward_matches_oracle(case, kernel, monkeypatch):
 @pytest.mark.parametrize("p", [0.6, 0.2])
 @pytest.mark.parametrize("kernel", ["default", "stored", "fwd_pipe"])
 def test_dropout_forward_and_backward(case, p, kernel, monkeypatch):
-    if kernel == "fwd_pipe":  # forward gathers pipelined one chunk ahead (U=16, V=2)
+    if kernel == "fwd_pipe":
+        # forward gathers pipelined one chunk ahead (U=16, V=2): the dropout /
+        # lse / y forward without kink sums (the kink-sum forward never pipelines)
+        monkeypatch.setenv("GAT_BWD_KINK", "0")
         monkeypatch.setenv("GAT_EDGE_PIPE", "1")
         monkeypatch.setenv("GAT_EDGE_U", "16")
         monkeypatch.setenv("GAT_EDGE_V", "2")
@@ -150,8 +153,9 @@ def test_dropout_forward_and_backward(case, p, kernel, monkeypatch):
 def test_kink_sums_backward_equals_edge_pass(shape, p, monkeypatch):
     """The kink-sum forward (gat_edge_aggregate_train) + gat_bwd_table give the
     gradients the edge-walking pass 1 (gat_edge_aggregate_ex + gat_bwd_targets,
-    GAT_BWD_KINK=0) gives, on the V = 1 (PPI) and pipelined V = 2 (Reddit)
-    kernels, and both match the float64 oracle."""
+    GAT_BWD_KINK=0) gives, on the V = 1 (PPI) and U = 16, V = 2 (Reddit)
+    kernels (the kink-sum forward unpipelined, the edge-pass forward pipelined
+    under GAT_EDGE_PIPE=1), and both match the float64 oracle."""
     if shape == "reddit_pipe":
         monkeypatch.setenv("GAT_EDGE_PIPE", "1")
         monkeypatch.setenv("GAT_EDGE_U", "16")
