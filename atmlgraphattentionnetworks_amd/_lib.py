@@ -18,7 +18,7 @@ GAT_OK = 0
 GAT_EINVAL = -1
 GAT_EUNSUPPORTED = -2
 GAT_EWORKSPACE = -3
-GAT_ABI_VERSION = 11
+GAT_ABI_VERSION = 12
 GAT_HINT_LOCAL = 1 << 30  # OR'd into edges_per_row_hint (include/gat_amd.h)
 GAT_HINT_SHORT = 1 << 29  # every row < 1024 in-edges (include/gat_amd.h, ABI 11)
 GAT_SEG_LOAD = 1
@@ -78,6 +78,11 @@ SIGNATURES = {
                                           _c_float, _c_u64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                           _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_dropout_seed_next": (_c_int, [_c_vp, _c_vp, _c_vp]),
+    "gat_csr_rotate": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp]),
+    "gat_csr_schedule_workspace_size": (_c_int, [_c_int, _c_size_p]),
+    "gat_csr_schedule": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
+                                  ctypes.c_size_t, _c_vp]),
+    "gat_csc_rotate": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp]),
     "gat_csc_workspace_size": (_c_int, [_c_ll, _c_int, _c_size_p]),
     "gat_csc_build": (_c_int, [_c_vp, _c_vp, _c_int, _c_ll, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                ctypes.c_size_t, _c_vp]),
@@ -176,6 +181,13 @@ def csr_workspace_size(num_edges: int, num_nodes: int) -> int:
     out = ctypes.c_size_t()
     check(load().gat_csr_workspace_size(num_edges, num_nodes, ctypes.byref(out)),
           "gat_csr_workspace_size")
+    return out.value
+
+
+def csr_schedule_workspace_size(num_nodes: int) -> int:
+    out = ctypes.c_size_t()
+    check(load().gat_csr_schedule_workspace_size(num_nodes, ctypes.byref(out)),
+          "gat_csr_schedule_workspace_size")
     return out.value
 
 

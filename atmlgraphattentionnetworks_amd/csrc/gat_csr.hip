@@ -146,6 +146,152 @@ size_t key_sort_tmp_bytes(long long count, unsigned bits) {
     return e == hipSuccess ? tmp : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Staggered row walks (gat_csr_rotate, gat_csr_schedule, gat_csc_rotate).  A row's
+// entries are sorted ascending (sources in a CSR row, targets in a CSC row);
+// the walk for schedule position p starts at the row's first entry >= start(p)
+// and wraps around: out[o + j] = in[b + (j + rot) mod d], rot = the number of
+// entries below start (a binary search).  One wave per row, lanes over its
+// entries (coalesced reads and writes).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int count_below(const int* __restrict__ v, int d, int x) {
+    int lo = 0, hi = d;  // first index with v[i] >= x
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (v[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ int walk_start(long long p, long long stride, int n) {
+    return stride > 0 ? (int)((p * stride) % (long long)n) : 0;
+}
+
+// rows at schedule positions p (row order[p], or p), written at out_off[p]
+// (the scheduled copy) or at the row's own CSR offset (out_off == nullptr)
+__global__ void k_rotate_rows(const int* __restrict__ rowptr, const int* __restrict__ in,
+                              const int* __restrict__ order, int n, long long stride,
+                              const int* __restrict__ out_off, int* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const long long waves = (long long)gridDim.x * (blockDim.x >> 6);
+    for (long long p = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); p < n;
+         p += waves) {
+        const int r = order != nullptr ? order[p] : (int)p;
+        const int b = rowptr[r], d = rowptr[r + 1] - b;
+        const int o = out_off != nullptr ? out_off[p] : b;
+        const int rot = stride > 0 ? count_below(in + b, d, walk_start(p, stride, n)) : 0;
+        for (int j = lane; j < d; j += 64) {
+            int jj = j + rot;
+            if (jj >= d) jj -= d;
+            out[o + j] = in[b + jj];
+        }
+    }
+}
+
+// the scheduled copy's segment bounds: deg_in_order[p] = degree of row order[p]
+__global__ void k_sched_degrees(const int* __restrict__ rowptr, const int* __restrict__ order,
+                                int n, int* __restrict__ deg) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) {
+        const int r = order[p];
+        deg[p] = rowptr[r + 1] - rowptr[r];
+    }
+}
+
+__global__ void k_sched_ends(const int* __restrict__ seg_b, int n, int* __restrict__ seg_e) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) seg_e[p] += seg_b[p];  // seg_e held the degrees
+}
+
+// a CSC row (source j, schedule position j) rotated: targets and edge ids
+// together, and the CSR-position -> CSC-slot map re-inverted
+__global__ void k_rotate_csc(const int* __restrict__ ptr, const int* __restrict__ dst,
+                             const int* __restrict__ eid, int n, long long stride,
+                             int* __restrict__ out_dst, int* __restrict__ out_eid,
+                             int* __restrict__ out_c2c) {
+    const int lane = threadIdx.x & 63;
+    const long long waves = (long long)gridDim.x * (blockDim.x >> 6);
+    for (long long j = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); j < n;
+         j += waves) {
+        const int b = ptr[j], d = ptr[j + 1] - b;
+        const int rot = stride > 0 ? count_below(dst + b, d, walk_start(j, stride, n)) : 0;
+        for (int t = lane; t < d; t += 64) {
+            int tt = t + rot;
+            if (tt >= d) tt -= d;
+            out_dst[b + t] = dst[b + tt];
+            if (eid != nullptr) {
+                const int k = eid[b + tt];
+                out_eid[b + t] = k;
+                if (out_c2c != nullptr) out_c2c[k] = b + t;
+            }
+        }
+    }
+}
+
+// exclusive scan of n ints (the scheduled copy's segment starts): 1024 per
+// block (256 threads x 4), the block totals scanned by one block with a carry,
+// then added back.  Small (n = the node count) and run once per graph.
+__device__ __forceinline__ int block_excl_scan256(int v, int* sh) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+        const int a = t >= off ? sh[t - off] : 0;
+        __syncthreads();
+        sh[t] += a;
+        __syncthreads();
+    }
+    const int incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_blocks(const int* __restrict__ in, int n,
+                                                     int* __restrict__ out,
+                                                     int* __restrict__ block_sums) {
+    __shared__ int sh[256];
+    const long long base = (long long)blockIdx.x * 1024 + threadIdx.x * 4;
+    int v[4], t = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[i] = base + i < n ? in[base + i] : 0;
+        t += v[i];
+    }
+    int run = block_excl_scan256(t, sh);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (base + i < n) out[base + i] = run;
+        run += v[i];
+    }
+    if (threadIdx.x == 255) block_sums[blockIdx.x] = run;
+}
+
+__global__ __launch_bounds__(256) void k_scan_sums(int* __restrict__ sums, int nb) {
+    __shared__ int sh[256];
+    int carry = 0;
+    for (int c0 = 0; c0 < nb; c0 += 256) {
+        const int i = c0 + threadIdx.x;
+        const int v = i < nb ? sums[i] : 0;
+        const int ex = block_excl_scan256(v, sh);
+        if (i < nb) sums[i] = carry + ex;
+        if (threadIdx.x == 255) sh[0] = ex + v;  // this chunk's total
+        __syncthreads();
+        carry += sh[0];
+        __syncthreads();
+    }
+}
+
+__global__ void k_scan_add(int* __restrict__ out, int n, const int* __restrict__ sums) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] += sums[i / 1024];
+}
+
+inline unsigned row_grid(long long rows) {  // 4 waves per block, capped grid
+    const long long blocks = (rows + 3) / 4;
+    return (unsigned)(blocks < 65536 ? (blocks > 0 ? blocks : 1) : 65536);
+}
+
 }  // namespace
 
 extern "C" {
@@ -254,6 +400,64 @@ int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nn
                        nnz, num_nodes, kn, csc_ptr);
     hipLaunchKernelGGL(k_csc_fill, dim3(grid_for(nnz, 256)), dim3(256), 0, st, keys_out, kn,
                        rowptr, num_nodes, nnz, csc_eid, csc_dst, csr_to_csc);
+    return status_of(hipGetLastError());
+}
+
+int gat_csr_rotate(const int* rowptr, const int* col, const int* row_order, int num_nodes,
+                   int stride, int* out_col, void* stream) {
+    if (num_nodes < 0 || stride < 0 || rowptr == nullptr || out_col == nullptr) return GAT_EINVAL;
+    if (num_nodes == 0) return GAT_OK;
+    if (row_order == nullptr) return GAT_EINVAL;  // (col, out_col: NULL with no entries)
+    hipLaunchKernelGGL(k_rotate_rows, dim3(row_grid(num_nodes)), dim3(256), 0,
+                       (hipStream_t)stream, rowptr, col, row_order, num_nodes, (long long)stride,
+                       nullptr, out_col);
+    return status_of(hipGetLastError());
+}
+
+int gat_csr_schedule_workspace_size(int num_nodes, size_t* bytes) {
+    if (num_nodes < 0 || bytes == nullptr) return GAT_EINVAL;
+    const size_t nb = ((size_t)num_nodes + 1023) / 1024;  // block totals of the scan
+    *bytes = align_up((nb > 0 ? nb : 1) * sizeof(int));
+    return GAT_OK;
+}
+
+int gat_csr_schedule(const int* rowptr, const int* col, const int* row_order, int num_nodes,
+                     int stagger, int* seg_begin, int* seg_end, int* out_col, void* workspace,
+                     size_t workspace_bytes, void* stream) {
+    if (num_nodes < 0 || stagger < 0) return GAT_EINVAL;
+    size_t need = 0;
+    int rc = gat_csr_schedule_workspace_size(num_nodes, &need);
+    if (rc != GAT_OK) return rc;
+    if (workspace_bytes < need) return GAT_EWORKSPACE;
+    if (num_nodes == 0) return GAT_OK;
+    if (rowptr == nullptr || row_order == nullptr || seg_begin == nullptr || seg_end == nullptr)
+        return GAT_EINVAL;  // (col, out_col: NULL with no entries)
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned g = (unsigned)((num_nodes + 255) / 256);
+    hipLaunchKernelGGL(k_sched_degrees, dim3(g), dim3(256), 0, st, rowptr, row_order, num_nodes,
+                       seg_end);
+    const int nb = (num_nodes + 1023) / 1024;
+    int* sums = (int*)workspace;
+    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(256), 0, st, seg_end, num_nodes, seg_begin,
+                       sums);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(256), 0, st, sums, nb);
+    hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(256), 0, st, seg_begin, num_nodes, sums);
+    hipLaunchKernelGGL(k_sched_ends, dim3(g), dim3(256), 0, st, seg_begin, num_nodes, seg_end);
+    hipLaunchKernelGGL(k_rotate_rows, dim3(row_grid(num_nodes)), dim3(256), 0, st, rowptr, col,
+                       row_order, num_nodes, (long long)stagger, seg_begin, out_col);
+    return status_of(hipGetLastError());
+}
+
+int gat_csc_rotate(const int* csc_ptr, const int* csc_dst, const int* csc_eid, int num_nodes,
+                   int stride, int* out_dst, int* out_eid, int* out_csr_to_csc, void* stream) {
+    if (num_nodes < 0 || stride < 0) return GAT_EINVAL;
+    if (num_nodes == 0) return GAT_OK;
+    if (csc_ptr == nullptr) return GAT_EINVAL;  // (csc_dst, out_dst: NULL with no entries)
+    if ((csc_eid == nullptr) != (out_eid == nullptr)) return GAT_EINVAL;
+    if (out_csr_to_csc != nullptr && csc_eid == nullptr) return GAT_EINVAL;
+    hipLaunchKernelGGL(k_rotate_csc, dim3(row_grid(num_nodes)), dim3(256), 0, (hipStream_t)stream,
+                       csc_ptr, csc_dst, csc_eid, num_nodes, (long long)stride, out_dst, out_eid,
+                       out_csr_to_csc);
     return status_of(hipGetLastError());
 }
 

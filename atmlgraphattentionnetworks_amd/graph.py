@@ -227,53 +227,39 @@ ROTATE_STRIDE = 2  # long rows: schedule position p's sweep starts at node 2p mo
 
 
 def build_sched_csr(csr: "CSRGraph", stagger: bool = False) -> SchedCSR:
-    """The scheduled copy.  ``stagger``: schedule position p's in-edges (sources
-    ascending) are rotated to start at the first source >= p and wrap around,
-    so the rows the kernel runs at one time sweep the node table from offsets
-    that advance with their position in the schedule (roughly their start
-    time) instead of all from node 0.  The same edges in another order:
-    results equal up to fp32 summation order."""
-    rp = csr.rowptr.to(torch.int64)
-    order = csr.order.to(torch.int64)
-    n = csr.num_nodes
-    deg = (rp[1:] - rp[:-1])[order]
-    sptr = torch.zeros(n + 1, dtype=torch.int64, device=rp.device)
-    sptr[1:] = deg.cumsum(0)
-    e = csr.num_edges  # output sizes given: no device -> host sync (graph-capture safe)
-    b_rep = torch.repeat_interleave(sptr[:-1], deg, output_size=e)
-    offs = torch.arange(e, device=rp.device) - b_rep
-    idx = torch.repeat_interleave(rp[order], deg, output_size=e) + offs
-    col = csr.col[idx]
-    if stagger and n > 0:
-        # (sources are node ids in [0, n): position p's sweep starts at node p)
-        pos = torch.repeat_interleave(torch.arange(n, device=rp.device), deg, output_size=e)
-        below = (col.to(torch.int64) < pos).to(torch.int64)
-        rot = torch.zeros(n, dtype=torch.int64, device=rp.device).index_add_(0, pos, below)
-        d_rep = torch.repeat_interleave(deg.clamp(min=1), deg, output_size=e)
-        col = col[b_rep + (offs + rot[pos]) % d_rep]
-    return SchedCSR(sptr[:-1].to(torch.int32).contiguous(), sptr[1:].to(torch.int32).contiguous(),
-                    col.contiguous())
+    """The scheduled copy (``gat_csr_schedule``).  ``stagger``: schedule position
+    p's in-edges (sources ascending) are rotated to start at the first source
+    >= p and wrap around, so the rows the kernel runs at one time sweep the
+    node table from offsets that advance with their position in the schedule
+    (roughly their start time) instead of all from node 0.  The same edges in
+    another order: results equal up to fp32 summation order."""
+    n, e = csr.num_nodes, csr.num_edges
+    dev = csr.rowptr.device
+    b = torch.empty(n, dtype=torch.int32, device=dev)
+    en = torch.empty(n, dtype=torch.int32, device=dev)
+    col = torch.empty(max(e, 1), dtype=torch.int32, device=dev)
+    ws = torch.empty(_lib.csr_schedule_workspace_size(n), dtype=torch.uint8, device=dev)
+    _lib.check(_lib.load().gat_csr_schedule(
+        csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.order.data_ptr(), n, 1 if stagger else 0,
+        b.data_ptr(), en.data_ptr(), col.data_ptr(), ws.data_ptr(), ws.numel(),
+        torch.cuda.current_stream(dev).cuda_stream), "gat_csr_schedule")
+    return SchedCSR(b, en, col[:e])
 
 
 def rotate_rows(csr: "CSRGraph", stride: int) -> torch.Tensor:
     """``csr.col`` with each row rotated to start at its first source >=
-    (schedule position * stride) mod N and wrap around: the rows the kernel
-    runs at one time then sweep the node table from offsets that advance with
-    their start time.  CSR row order kept (so ``rowptr`` and the hub schedule
-    still index it); the same edges in another order within each row."""
-    rp = csr.rowptr.to(torch.int64)
-    n, e = csr.num_nodes, csr.num_edges
-    dev = rp.device
-    pos = torch.empty(n, dtype=torch.int64, device=dev)
-    pos[csr.order.to(torch.int64)] = torch.arange(n, device=dev)
-    deg = rp[1:] - rp[:-1]
-    row = torch.repeat_interleave(torch.arange(n, device=dev), deg, output_size=e)
-    start = (pos * stride) % n
-    below = (csr.col.to(torch.int64) < start[row]).to(torch.int64)
-    rot = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, row, below)
-    base = rp[:-1][row]
-    offs = torch.arange(e, device=dev) - base
-    return csr.col[base + (offs + rot[row]) % deg.clamp(min=1)[row]].contiguous()
+    (schedule position * stride) mod N and wrap around (``gat_csr_rotate``):
+    the rows the kernel runs at one time then sweep the node table from
+    offsets that advance with their start time.  CSR row order kept (so
+    ``rowptr`` and the hub schedule still index it); the same edges in another
+    order within each row."""
+    dev = csr.rowptr.device
+    out = torch.empty(max(csr.num_edges, 1), dtype=torch.int32, device=dev)
+    _lib.check(_lib.load().gat_csr_rotate(
+        csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.order.data_ptr(), csr.num_nodes,
+        int(stride), out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream),
+        "gat_csr_rotate")
+    return out[:csr.num_edges]
 
 
 _sched_cache = {}
@@ -407,25 +393,18 @@ def rotate_csc(csc: CSCGraph, n: int, e: int, stride: int) -> CSCGraph:
     """Staggered sweeps for the backward source pass (``gat_bwd_sources`` walks
     source rows in node order): source j's CSC slots rotated to start at its
     first target >= stride * j mod N and wrap around, ``dst`` and ``eid``
-    together, ``csr_to_csc`` re-inverted.  The same out-edges per source in
-    another order (gradients equal up to fp32 summation order).  Reddit
-    training step (dropout 0.6) 8.65 -> 8.46 ms at stride 8; strides 1 / 2 /
-    4 / 16 / 64: 8.59 / 8.60 / 8.49 / 8.61 / 9.04 ms
+    together, ``csr_to_csc`` re-inverted (``gat_csc_rotate``).  The same
+    out-edges per source in another order (gradients equal up to fp32
+    summation order).  Reddit training step (dropout 0.6) 8.65 -> 8.46 ms at
+    stride 8; strides 1 / 2 / 4 / 16 / 64: 8.59 / 8.60 / 8.49 / 8.61 / 9.04 ms
     (profiles/r06/train_ab_csc_rotate_reddit.json)."""
-    ptr = csc.ptr.to(torch.int64)
-    dev = ptr.device
-    deg = ptr[1:] - ptr[:-1]
-    row = torch.repeat_interleave(torch.arange(n, device=dev), deg, output_size=e)
-    start = (torch.arange(n, device=dev) * stride) % max(n, 1)
-    below = (csc.dst.to(torch.int64) < start[row]).to(torch.int64)
-    rot = torch.zeros(n, dtype=torch.int64, device=dev).index_add_(0, row, below)
-    base = ptr[:-1][row]
-    src = base + (torch.arange(e, device=dev) - base + rot[row]) % deg.clamp(min=1)[row]
-    del row, start, below, base
-    eid = csc.eid[src].contiguous()
-    c2c = torch.empty_like(csc.csr_to_csc)
-    c2c[eid.to(torch.int64)] = torch.arange(e, device=dev, dtype=torch.int32)
-    return CSCGraph(csc.ptr, csc.dst[src].contiguous(), eid, c2c)
+    dev = csc.ptr.device
+    out = torch.empty(3, max(e, 1), dtype=torch.int32, device=dev)
+    _lib.check(_lib.load().gat_csc_rotate(
+        csc.ptr.data_ptr(), csc.dst.data_ptr(), csc.eid.data_ptr(), n, int(stride),
+        out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
+        torch.cuda.current_stream(dev).cuda_stream), "gat_csc_rotate")
+    return CSCGraph(csc.ptr, out[0, :e], out[1, :e], out[2, :e])
 
 
 def get_csc(csr: CSRGraph) -> CSCGraph:

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GAT_ABI_VERSION 11
+#define GAT_ABI_VERSION 12
 
 #define GAT_OK 0
 #define GAT_EINVAL (-1)       /* malformed arguments (negative sizes, bad layout) */
@@ -390,6 +390,44 @@ int gat_edge_aggregate_train(const int* rowptr, const int* col, const int* row_o
  */
 int gat_dropout_seed_next(unsigned long long* counter, unsigned long long* seed_out,
                           void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Staggered row walks (ABI 12).  The edge entry points take a row's in-edges
+ * in any order; walking each row from its first source at or after a start
+ * that advances with the row's schedule position, and wrapping around, keeps
+ * the rows that run together from all gathering the same table lines at once
+ * (PPI edge kernel 3-4% faster, Reddit layer 2.6%).  All three are stateless
+ * device passes on `stream` over rows whose entries ascend (gat_csr_build's
+ * col, gat_csc_build's csc_dst); position p's start is (p * stride) mod N.
+ * ------------------------------------------------------------------------- */
+
+/* out_col [nnz]: col with row row_order[p] rotated for start (p * stride) mod N,
+ * in CSR order (rowptr still indexes it).  The module's eval forward walks it at
+ * stride 2 when rows average >= 64 in-edges.  stride = 0 copies col. */
+int gat_csr_rotate(const int* rowptr, const int* col, const int* row_order, int num_nodes,
+                   int stride, int* out_col, void* stream);
+
+/* Workspace bytes gat_csr_schedule needs (a device scan). */
+int gat_csr_schedule_workspace_size(int num_nodes, size_t* bytes);
+
+/* The scheduled CSR copy: position p holds row row_order[p]'s entries at
+ * [seg_begin[p], seg_end[p]) of out_col, positions contiguous in order (the
+ * seg_begin/seg_end/col arguments of gat_edge_aggregate_seg and
+ * gat_layer_forward with seg_by_pos = 1).  stagger = 0: each row as in col;
+ * stagger = s > 0: rotated for start (p * s) mod N (the module uses 1 when rows
+ * average 16-63 in-edges). */
+int gat_csr_schedule(const int* rowptr, const int* col, const int* row_order, int num_nodes,
+                     int stagger, int* seg_begin, int* seg_end, int* out_col, void* workspace,
+                     size_t workspace_bytes, void* stream);
+
+/* The CSC with source j's slots rotated for start (j * stride) mod N: csc_dst
+ * and csc_eid (optional) permuted together, and out_csr_to_csc (optional,
+ * needs csc_eid) the inverse of the permuted eid.  The module's backward uses
+ * stride 8 when rows average >= 64 in-edges (gradients equal up to fp32
+ * summation order).  In all three the entry arrays may be NULL when the graph
+ * has no entries. */
+int gat_csc_rotate(const int* csc_ptr, const int* csc_dst, const int* csc_eid, int num_nodes,
+                   int stride, int* out_dst, int* out_eid, int* out_csr_to_csc, void* stream);
 
 /* Workspace bytes gat_csc_build needs for nnz = E + N CSR entries. */
 int gat_csc_workspace_size(long long nnz, int num_nodes, size_t* bytes);
