@@ -50,6 +50,7 @@ L2_GATHER_CEILING_GBS = 18800.0
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (v_mfma_f32_16x16x4_f32)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 matrix peak (v_mfma_f32_16x16x32_bf16)
 SPLIT_PRODUCTS = 6  # bf16 MFMA products per fp32 product in the split-bf16 projections
+_PROCESS_WARMUP_MS = None  # the first graph build of the process (one-time costs)
 
 
 def projection_kernel(fin: int, f: int = 8) -> dict:
@@ -245,14 +246,23 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
     layer = GraphAttentionLayer(w.in_channels, w.out_channels, num_heads=w.heads,
                                 concat=w.concat).to(dev).eval()
     torch.cuda.synchronize()
+    # the process's first graph build also pays one-time costs: the load of the
+    # library's GPU code objects (the first launch from each of libgat_amd.so's
+    # modules) and torch's first-use allocations.  A 64-node graph takes them
+    # (reported as csr_process_warmup_ms), so csr_build_once is this graph's
+    # first build in a warmed process
+    from atmlgraphattentionnetworks_amd.graph import build_csr
+    global _PROCESS_WARMUP_MS
+    if _PROCESS_WARMUP_MS is None:
+        t0 = time.perf_counter()
+        build_csr(torch.randint(0, 64, (2, 256), device=dev), 64)
+        torch.cuda.synchronize()
+        _PROCESS_WARMUP_MS = (time.perf_counter() - t0) * 1e3
     t0 = time.perf_counter()
     csr = get_csr(ei, n)
     torch.cuda.synchronize()
     csr_ms = (time.perf_counter() - t0) * 1e3
-    # the same build again: the first one in a process also pays the one-time
-    # load of the library's GPU code objects (the first launch from each of
-    # libgat_amd.so's modules) and torch's first-use allocations
-    from atmlgraphattentionnetworks_amd.graph import build_csr
+    # the same build again (every buffer allocated before: the build's own time)
     t0 = time.perf_counter()
     build_csr(ei, n)
     torch.cuda.synchronize()
@@ -352,6 +362,7 @@ def measure_workload(name: str, dev, steps: int, warmup: int, edge_iters: int,
         "value": e_prime / (ms * 1e-3), "unit": "edges/s", "ms_per_step": ms, "launch": launch,
         "ms_per_step_graph": ms_graph,
         "csr_build_once_ms": csr_ms, "csr_build_warm_ms": csr_warm_ms,
+        "csr_process_warmup_ms": _PROCESS_WARMUP_MS,
         "phases_in_step_ms": None if fused else in_step,
         "edge_kernel": {
             "kernel": ("k_edge_grp<..., XF> with the projection fused (gat_layer_forward, "
@@ -832,6 +843,7 @@ def main():
         "breakdown_ms": {"project": head["projection"]["ms"], "edge": head["edge_kernel"]["ms"],
                          "csr_build_once": head["csr_build_once_ms"],
                          "csr_build_warm": head["csr_build_warm_ms"],
+                         "csr_process_warmup": head["csr_process_warmup_ms"],
                          "in_step": {k: v for k, v in (head.get("phases_in_step_ms") or {}).items()
                                      if k != "what"}},
         "projection": {"bound": "mfma", "kernel": head["projection"]["kernel"],
