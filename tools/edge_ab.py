@@ -223,6 +223,7 @@ def main():
         env = dict(env)
         from atmlgraphattentionnetworks_amd import graph as _graph
         _graph._sched_cache.clear()  # the scheduled copy is built under each variant's knobs
+        _graph._rot_cache.clear()  # and the rotated col
         if int(env.pop("hublast", "0")):
             apply(env)
             plan = ForwardPlan(x, csr, w.heads, w.out_channels, w.concat, 0.2)
