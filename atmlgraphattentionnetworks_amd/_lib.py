@@ -78,7 +78,7 @@ SIGNATURES = {
                                           _c_float, _c_u64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                           _c_vp, _c_vp, _c_int, _c_vp]),
     "gat_dropout_seed_next": (_c_int, [_c_vp, _c_vp, _c_vp]),
-    "gat_csr_rotate": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp]),
+    "gat_csr_rotate": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int, _c_vp, _c_vp]),
     "gat_csr_schedule_workspace_size": (_c_int, [_c_int, _c_size_p]),
     "gat_csr_schedule": (_c_int, [_c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                                   ctypes.c_size_t, _c_vp]),

@@ -172,7 +172,8 @@ __device__ __forceinline__ int walk_start(long long p, long long stride, int n) 
 // (the scheduled copy) or at the row's own CSR offset (out_off == nullptr)
 __global__ void k_rotate_rows(const int* __restrict__ rowptr, const int* __restrict__ in,
                               const int* __restrict__ order, int n, long long stride,
-                              const int* __restrict__ out_off, int* __restrict__ out) {
+                              int max_degree, const int* __restrict__ out_off,
+                              int* __restrict__ out) {
     const int lane = threadIdx.x & 63;
     const long long waves = (long long)gridDim.x * (blockDim.x >> 6);
     for (long long p = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); p < n;
@@ -180,7 +181,8 @@ __global__ void k_rotate_rows(const int* __restrict__ rowptr, const int* __restr
         const int r = order != nullptr ? order[p] : (int)p;
         const int b = rowptr[r], d = rowptr[r + 1] - b;
         const int o = out_off != nullptr ? out_off[p] : b;
-        const int rot = stride > 0 ? count_below(in + b, d, walk_start(p, stride, n)) : 0;
+        const bool turn = stride > 0 && (max_degree <= 0 || d <= max_degree);
+        const int rot = turn ? count_below(in + b, d, walk_start(p, stride, n)) : 0;
         for (int j = lane; j < d; j += 64) {
             int jj = j + rot;
             if (jj >= d) jj -= d;
@@ -404,13 +406,13 @@ int gat_csc_build(const int* rowptr, const int* col, int num_nodes, long long nn
 }
 
 int gat_csr_rotate(const int* rowptr, const int* col, const int* row_order, int num_nodes,
-                   int stride, int* out_col, void* stream) {
+                   int stride, int max_degree, int* out_col, void* stream) {
     if (num_nodes < 0 || stride < 0 || rowptr == nullptr || out_col == nullptr) return GAT_EINVAL;
     if (num_nodes == 0) return GAT_OK;
     if (row_order == nullptr) return GAT_EINVAL;  // (col, out_col: NULL with no entries)
     hipLaunchKernelGGL(k_rotate_rows, dim3(row_grid(num_nodes)), dim3(256), 0,
                        (hipStream_t)stream, rowptr, col, row_order, num_nodes, (long long)stride,
-                       nullptr, out_col);
+                       max_degree, nullptr, out_col);
     return status_of(hipGetLastError());
 }
 
@@ -444,7 +446,7 @@ int gat_csr_schedule(const int* rowptr, const int* col, const int* row_order, in
     hipLaunchKernelGGL(k_scan_add, dim3(g), dim3(256), 0, st, seg_begin, num_nodes, sums);
     hipLaunchKernelGGL(k_sched_ends, dim3(g), dim3(256), 0, st, seg_begin, num_nodes, seg_end);
     hipLaunchKernelGGL(k_rotate_rows, dim3(row_grid(num_nodes)), dim3(256), 0, st, rowptr, col,
-                       row_order, num_nodes, (long long)stagger, seg_begin, out_col);
+                       row_order, num_nodes, (long long)stagger, 0, seg_begin, out_col);
     return status_of(hipGetLastError());
 }
 

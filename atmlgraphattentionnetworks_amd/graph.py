@@ -246,18 +246,20 @@ def build_sched_csr(csr: "CSRGraph", stagger: bool = False) -> SchedCSR:
     return SchedCSR(b, en, col[:e])
 
 
-def rotate_rows(csr: "CSRGraph", stride: int) -> torch.Tensor:
+def rotate_rows(csr: "CSRGraph", stride: int, max_degree: int = 0) -> torch.Tensor:
     """``csr.col`` with each row rotated to start at its first source >=
     (schedule position * stride) mod N and wrap around (``gat_csr_rotate``):
     the rows the kernel runs at one time then sweep the node table from
     offsets that advance with their start time.  CSR row order kept (so
     ``rowptr`` and the hub schedule still index it); the same edges in another
-    order within each row."""
+    order within each row.  Rows of more than ``max_degree`` (> 0) in-edges are
+    copied unrotated."""
     dev = csr.rowptr.device
     out = torch.empty(max(csr.num_edges, 1), dtype=torch.int32, device=dev)
     _lib.check(_lib.load().gat_csr_rotate(
         csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.order.data_ptr(), csr.num_nodes,
-        int(stride), out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream),
+        int(stride), int(max_degree), out.data_ptr(),
+        torch.cuda.current_stream(dev).cuda_stream),
         "gat_csr_rotate")
     return out[:csr.num_edges]
 
@@ -281,7 +283,11 @@ def rotated_col(csr: "CSRGraph") -> torch.Tensor:
     hit = _rot_cache.get(key)
     if hit is not None and hit[0]() is csr.rowptr:
         return hit[1]
-    col = rotate_rows(csr, ROTATE_STRIDE)
+    # hub rows (split into segments scheduled by the first source each
+    # gathers) stay ascending: power-law Reddit 2.238 -> 2.229 ms
+    # (profiles/r06/step_ab_hub_rows_unrotated_powerlaw.json)
+    hubs = csr.hubs
+    col = rotate_rows(csr, ROTATE_STRIDE, 2 * hubs.seg_len if hubs is not None else 0)
     _rot_cache[key] = (weakref.ref(csr.rowptr), col)
     weakref.finalize(csr.rowptr, _rot_cache.pop, key, None)
     return col

@@ -403,9 +403,11 @@ int gat_dropout_seed_next(unsigned long long* counter, unsigned long long* seed_
 
 /* out_col [nnz]: col with row row_order[p] rotated for start (p * stride) mod N,
  * in CSR order (rowptr still indexes it).  The module's eval forward walks it at
- * stride 2 when rows average >= 64 in-edges.  stride = 0 copies col. */
+ * stride 2 when rows average >= 64 in-edges.  stride = 0 copies col; rows of more
+ * than max_degree entries (> 0) are copied unrotated (the module passes its hub
+ * threshold: hub segments are scheduled by the first source they gather). */
 int gat_csr_rotate(const int* rowptr, const int* col, const int* row_order, int num_nodes,
-                   int stride, int* out_col, void* stream);
+                   int stride, int max_degree, int* out_col, void* stream);
 
 /* Workspace bytes gat_csr_schedule needs (a device scan). */
 int gat_csr_schedule_workspace_size(int num_nodes, size_t* bytes);

@@ -69,6 +69,21 @@ def test_rotated_rows_keep_csr_order(stride):
 
 
 @pytest.mark.gpu
+def test_rotated_rows_skip_rows_past_max_degree():
+    """max_degree > 0: rows with more entries stay as they are (the hub rows,
+    whose segments are scheduled by the first source they gather)."""
+    csr = _csr(300, 9000, 11, "cuda")
+    rp, col, order = csr.rowptr.cpu().numpy(), csr.col.cpu().numpy(), csr.order.cpu().numpy()
+    deg = np.diff(rp)
+    cap = int(np.median(deg))
+    rot = rotate_rows(csr, 3, cap).cpu().numpy()
+    for p, r in enumerate(order):
+        row = col[rp[r]:rp[r + 1]]
+        want = row if deg[r] > cap else _rot(row, (3 * p) % csr.num_nodes)
+        assert (rot[rp[r]:rp[r + 1]] == want).all(), p
+
+
+@pytest.mark.gpu
 def test_rotated_col_only_for_long_rows(monkeypatch):
     """Long rows: a cached rotated copy at ROTATE_STRIDE; GAT_EDGE_SCHED=plain
     turns it off."""
